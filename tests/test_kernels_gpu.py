@@ -1,0 +1,89 @@
+"""Numerics of the HIP kernels vs the fp32 PyTorch reference (mift.ops.reference)."""
+import pytest
+import torch
+
+import mift
+from mift.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    assert mift.kernels_available(), f"extension not loaded: {mift._ext.error()!r}"
+    import mift._C as C
+    return C
+
+
+@pytest.mark.parametrize("D", [64, 768, 2560, 4096])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_layer_norm_fwd_bwd(D, dt):
+    C = _C()
+    torch.manual_seed(0)
+    M = 300
+    x = torch.randn(M, D, device="cuda", dtype=dt)
+    w = (1 + 0.1 * torch.randn(D, device="cuda")).to(dt)
+    b = (0.1 * torch.randn(D, device="cuda")).to(dt)
+    y, mean, rstd = C.layer_norm_fwd(x, w, b, 1e-5)
+    xr = x.float().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), w.float(), b.float(), 1e-5)
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy = torch.randn_like(x)
+    dres = torch.randn_like(x)
+    yr.backward(dy.float())
+    dx, dbr, dw, db = C.layer_norm_bwd(dy, x, w, mean, rstd, dres, True, 0.1, 1234, False)
+    exp = xr.grad + dres.float()
+    torch.testing.assert_close(dx.float(), exp, atol=5e-2, rtol=3e-2)
+    mask = ref.keep_mask(1234, (M, D), 0.1, device="cuda")
+    torch.testing.assert_close(dbr.float(), torch.where(mask, dx.float() / 0.9, torch.zeros_like(exp)),
+                               atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 2304, 768), (8192, 768, 3072), (130, 200, 128)])
+def test_gemm_nt_plain(M, N, K):
+    C = _C()
+    torch.manual_seed(1)
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    out = C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0)[0]
+    exp = a.float() @ b.float().t()
+    torch.testing.assert_close(out.float(), exp, atol=3e-2, rtol=2e-2)
+
+
+def test_gemm_nt_identity_asymmetric():
+    """A = I with an asymmetric B catches swapped C/D layouts (guide §3)."""
+    C = _C()
+    n = 128
+    a = torch.eye(n, device="cuda", dtype=torch.bfloat16)
+    bm = (torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
+    out = C.gemm_nt(a, bm, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0)[0]
+    torch.testing.assert_close(out.float(), bm.float().t())
+
+
+@pytest.mark.parametrize("act", [1, 2])
+def test_gemm_nt_fused_epilogue(act):
+    C = _C()
+    torch.manual_seed(2)
+    M, N, K = 512, 384, 256
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
+    b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    out, pre = C.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True, 1.0, None, 0)
+    exp, exp_pre = ref.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True)
+    torch.testing.assert_close(pre.float(), exp_pre.float(), atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(out.float(), exp.float(), atol=8e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("act", [4, 5])
+def test_gemm_nt_act_backward(act):
+    C = _C()
+    torch.manual_seed(3)
+    M, N, K = 256, 512, 128
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    aux = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    out = C.gemm_nt(a, b, None, None, None, act, aux, None, 0.0, 0, False, 1.0, None, 0)[0]
+    exp, _ = ref.gemm_nt(a, b, None, None, None, act, aux)
+    torch.testing.assert_close(out.float(), exp.float(), atol=5e-2, rtol=3e-2)

@@ -1,0 +1,106 @@
+"""Micro-benchmarks of the mift HIP kernels vs the torch/hipBLASLt equivalent.
+
+Usage:  python tools/bench_kernels.py [--only gemm,ln,attn,xent] [--json out.json]
+Timing: CUDA events around `iters` back-to-back launches after warmup, on
+random data (guide §5.4 rule 25), median of 5 rounds, both variants
+interleaved in one process (rule 24).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import mift  # noqa: E402
+
+
+def timeit(fn, iters=20, rounds=5):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e) / iters)
+    return statistics.median(ts)
+
+
+GEMM_SHAPES = [
+    # (name, M, N, K)  distilgpt2, 32x256 tokens per rank
+    ("c_attn.fwd", 8192, 2304, 768),
+    ("attn.c_proj.fwd", 8192, 768, 768),
+    ("mlp.c_fc.fwd", 8192, 3072, 768),
+    ("mlp.c_proj.fwd", 8192, 768, 3072),
+    ("c_attn.dgrad", 8192, 768, 2304),
+    ("mlp.c_fc.dgrad", 8192, 768, 3072),
+    ("mlp.c_proj.dgrad", 8192, 3072, 768),
+    ("lm_head.fwd", 8192, 50304, 768),
+    ("lm_head.dgrad", 8192, 768, 50304),
+    # OPT-2.7B, 4x512 tokens per micro-batch
+    ("opt.qkv.fwd", 2048, 7680, 2560),
+    ("opt.fc1.fwd", 2048, 10240, 2560),
+    ("opt.fc2.fwd", 2048, 2560, 10240),
+    ("square4k", 4096, 4096, 4096),
+]
+
+
+def bench_gemm(results):
+    import mift._C as C
+    for name, M, N, K in GEMM_SHAPES:
+        a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+        fl = 2.0 * M * N * K
+        row = {"name": name, "M": M, "N": N, "K": K}
+        for tile in (0, 1, 2, 3):
+            t = timeit(lambda: C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, tile))
+            row[f"mift_t{tile}_ms"] = round(t, 4)
+            row[f"mift_t{tile}_tflops"] = round(fl / t / 1e9, 1)
+        t = timeit(lambda: torch.matmul(a, b.t()))
+        row["torch_ms"] = round(t, 4)
+        row["torch_tflops"] = round(fl / t / 1e9, 1)
+        print(json.dumps(row), flush=True)
+        results.append(row)
+
+
+def bench_ln(results):
+    import mift._C as C
+    for M, D in [(8192, 768), (2048, 2560), (8192, 4096)]:
+        x = torch.randn(M, D, device="cuda", dtype=torch.bfloat16)
+        w = torch.ones(D, device="cuda", dtype=torch.bfloat16)
+        b = torch.zeros(D, device="cuda", dtype=torch.bfloat16)
+        t = timeit(lambda: C.layer_norm_fwd(x, w, b, 1e-5))
+        tt = timeit(lambda: torch.nn.functional.layer_norm(x, (D,), w, b, 1e-5))
+        gbs = 2 * x.numel() * 2 / t / 1e6
+        row = {"name": f"ln_fwd_{M}x{D}", "mift_ms": round(t, 4), "mift_GBps": round(gbs, 1),
+               "torch_ms": round(tt, 4)}
+        print(json.dumps(row), flush=True)
+        results.append(row)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="gemm,ln")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    assert mift.kernels_available(), mift._ext.error()
+    results = []
+    for k in a.only.split(","):
+        {"gemm": bench_gemm, "ln": bench_ln}[k](results)
+    if a.json:
+        os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
+        with open(a.json, "w") as f:
+            json.dump(results, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,117 @@
+// Shared device helpers for the mift gfx950 kernels.
+//
+// Conventions (all kernels):
+//   * wave64: lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+//   * 16-bit element types are clang's native __bf16 / _Float16 (gfx950 has
+//     hardware converts: v_cvt_pk_bf16_f32), accumulation is always fp32;
+//   * dropout masks are counter-based (no mask tensors are stored): element
+//     `idx` of a call with seed `s` is kept iff mift_hash(s, idx) >= thr,
+//     thr = p * 2^32.  mift.ops.reference re-implements the same hash in
+//     torch so CPU tests reproduce the GPU mask bit for bit, and recompute
+//     (activation checkpointing) regenerates identical masks.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MIFT_HD __device__ __forceinline__
+
+typedef __bf16 bf16;
+typedef _Float16 fp16;
+
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef short short4_ __attribute__((ext_vector_type(4)));
+typedef float float4_ __attribute__((ext_vector_type(4)));
+typedef float float16_ __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 fp16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T> MIFT_HD float to_f32(T x) { return (float)x; }
+template <typename T> MIFT_HD T from_f32(float x) { return (T)x; }
+
+// splitmix64 finaliser of (seed + idx * golden) -> top 32 bits.
+MIFT_HD uint32_t mift_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+MIFT_HD bool mift_keep(uint64_t seed, uint64_t idx, uint32_t thr) { return mift_hash(seed, idx) >= thr; }
+
+// GPT-2 "gelu_new" (tanh approximation) and its derivative.
+MIFT_HD float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+MIFT_HD float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+MIFT_HD float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+MIFT_HD float gelu_erf_grad(float x) {
+  float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// wave64 reductions (DPP/shuffle handled by the compiler for __shfl_xor).
+MIFT_HD float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+MIFT_HD float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blocks of NW waves; `scratch` needs NW floats of LDS.
+template <int NW>
+MIFT_HD float block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (NW == 1) return v;
+  __syncthreads();
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r += scratch[i];
+  return r;
+}
+
+// Vector load/store of 8 16-bit elements (16 B per lane, Guideline 13).
+template <typename T>
+MIFT_HD void load8(const T* p, float* out) {
+  short8 v = *reinterpret_cast<const short8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    short s = v[i];
+    T t;
+    __builtin_memcpy(&t, &s, 2);
+    out[i] = (float)t;
+  }
+}
+template <typename T>
+MIFT_HD void store8(T* p, const float* in) {
+  short8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    T t = (T)in[i];
+    short s;
+    __builtin_memcpy(&s, &t, 2);
+    v[i] = s;
+  }
+  *reinterpret_cast<short8*>(p) = v;
+}
+
+#define MIFT_CHECK_HIP(expr)                                                        \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    TORCH_CHECK(_e == hipSuccess, "HIP error: ", hipGetErrorString(_e), " at ", #expr); \
+  } while (0)

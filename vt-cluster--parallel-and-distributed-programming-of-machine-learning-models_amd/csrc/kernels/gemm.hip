@@ -1,0 +1,357 @@
+// K1/K2: bf16/fp16 MFMA GEMM "NT" with fused epilogues.
+//
+//   C[M,N] = epi( A[M,K] · B[N,K]^T  (+ A2[M,32] · B2[N,32]^T) )
+//
+// Both operands are K-contiguous ("NT"), the layout the gfx950 MFMA
+// fragments want: a 16x16x32 A or B fragment is 8 consecutive K elements of
+// one row = one 16-byte ds_read_b128.  Frozen base weights are stored once
+// per orientation (W as [out,in] for forward, W^T as [in,out] for dgrad),
+// so forward and dgrad are both this kernel (see mift/ops/linear.py).
+//
+// The optional A2/B2 pair is the LoRA "K-extension": with
+// T = s·dropout(X)·A^T (rank r<=32, zero padded to 32 columns) and
+// B2 = B (padded to [N,32]), one extra MFMA K-step adds the low-rank update
+// s·dropout(X)·A^T·B^T to the same accumulators as X·W^T — the adapter
+// costs one MFMA per output fragment instead of a second GEMM + add.
+//
+// Tiling (gfx950): 256 threads = 4 waves (2x2), block tile BM x BN x 64,
+// each wave owns (BM/2) x (BN/2) as 16x16 MFMA tiles (mfma_f32_16x16x32).
+// Global->LDS staging by global_load_lds_dwordx4 (no VGPR round trip) into a
+// double-buffered, XOR-swizzled image (16-B chunk c of row r stored at chunk
+// c ^ (r & 7)) which makes every ds_read_b128 fragment read conflict-free
+// (checked with the lane-group model of the gfx950 LDS).  The swizzle is
+// applied on the per-lane global SOURCE address because the LDS-DMA
+// destination is lane-linear (guide rule 21).
+//
+// Epilogue (two phases): accumulators (+bias) -> bf16 tile in LDS, then
+// every thread streams 8 consecutive columns (16-B loads/stores) applying
+// the elementwise tail: activation (gelu_new / relu / gelu_erf) with an
+// optional pre-activation output, activation-backward (dZ = dY ⊙ act'(z)),
+// dropout (counter hash, see common.h) and residual add.
+//
+// Block order is XCD-aware (bijective remap, guide T1): blocks that share
+// an XCD (b, b+8, ...) walk the N tiles of the same A row panel.
+#include "common.h"
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+namespace {
+
+enum Act : int {
+  ACT_NONE = 0,
+  ACT_GELU_TANH = 1,
+  ACT_RELU = 2,
+  ACT_GELU_ERF = 3,
+  ACT_GELU_TANH_BWD = 4,  // out = acc * gelu_tanh'(aux)
+  ACT_RELU_BWD = 5,       // out = acc * (aux > 0)
+  ACT_GELU_ERF_BWD = 6,
+};
+
+struct EpiArgs {
+  const void* bias;  // [N] (T or float)
+  int bias_f32;
+  const void* aux;   // [M,N] T (pre-activation for *_BWD)
+  void* preact;      // [M,N] T (store z before activation)
+  const void* residual;  // [M,N] T: out = residual + dropout(act(z))
+  int act;
+  uint64_t seed;
+  uint32_t thr;      // dropout threshold (0 = no dropout)
+  float inv_keep;
+  float alpha;       // acc scale
+};
+
+template <typename T>
+using frag_t = typename std::conditional<std::is_same<T, bf16>::value, bf16x8, fp16x8>::type;
+
+template <typename T>
+MIFT_HD float4_ mfma16(frag_t<T> a, frag_t<T> b, float4_ c) {
+  if constexpr (std::is_same<T, bf16>::value)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+MIFT_HD float apply_act(int act, float z, float aux) {
+  switch (act) {
+    case ACT_GELU_TANH: return gelu_tanh(z);
+    case ACT_RELU: return fmaxf(z, 0.f);
+    case ACT_GELU_ERF: return gelu_erf(z);
+    case ACT_GELU_TANH_BWD: return z * gelu_tanh_grad(aux);
+    case ACT_RELU_BWD: return aux > 0.f ? z : 0.f;
+    case ACT_GELU_ERF_BWD: return z * gelu_erf_grad(aux);
+    default: return z;
+  }
+}
+
+constexpr int BK = 64;
+constexpr int ROWB = BK * 2;  // bytes per LDS row (128)
+
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                         T* __restrict__ C, const T* __restrict__ A2,
+                                                         const T* __restrict__ B2, int M, int N, int K,
+                                                         int lda, int ldb, int ldc, EpiArgs ep) {
+  constexpr int WM = BM / 2, WN = BN / 2;      // wave tile
+  constexpr int TM = WM / 16, TN = WN / 16;    // MFMA tiles per wave
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- XCD-aware bijective block remap (T1) ----
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
+  const int nblk = ntm * ntn;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r = nblk % 8;
+    const int xcd = bid % 8, loc = bid / 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- staging: each wave-instruction writes 1 KiB = 8 rows x 128 B ----
+  // lane -> (row-in-8 = lane>>3, physical chunk = lane&7); logical chunk =
+  // physical ^ (row & 7) -> per-lane source address.
+  auto stage = [&](int buf, int k0) {
+    char* base = smem + buf * STAGE_BYTES;
+    constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;  // per tile
+#pragma unroll
+    for (int i = wave; i < A_INSTR; i += 4) {
+      int r = i * 8 + (lane >> 3);
+      int pc = lane & 7;
+      int lc = pc ^ (r & 7);
+      int gr = min(m0 + r, M - 1);
+      const T* src = A + (size_t)gr * lda + k0 + lc * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + i * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = wave; i < B_INSTR; i += 4) {
+      int r = i * 8 + (lane >> 3);
+      int pc = lane & 7;
+      int lc = pc ^ (r & 7);
+      int gr = min(n0 + r, N - 1);
+      const T* src = B + (size_t)gr * ldb + k0 + lc * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + A_BYTES + i * 1024), 16, 0, 0);
+    }
+  };
+
+  float4_ acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage(0, 0);
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0)
+  __syncthreads();
+
+  const int fr = lane & 15;      // fragment row
+  const int fq = lane >> 4;      // k sub-chunk (0..3)
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    const char* As = smem + cur * STAGE_BYTES;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int lc = kk * 4 + fq;
+      frag_t<T> af[TM], bfv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int r = wm * WM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const frag_t<T>*>(As + r * ROWB + ((lc ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int r = wn * WN + j * 16 + fr;
+        bfv[j] = *reinterpret_cast<const frag_t<T>*>(Bs + r * ROWB + ((lc ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(af[i], bfv[j], acc[i][j]);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- LoRA K-extension: one extra K=32 step from global (A2[M,32], B2[N,32]) ----
+  if (A2 != nullptr) {
+    frag_t<T> af[TM], bfv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int r = min(m0 + wm * WM + i * 16 + fr, M - 1);
+      af[i] = *reinterpret_cast<const frag_t<T>*>(A2 + (size_t)r * 32 + fq * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int r = min(n0 + wn * WN + j * 16 + fr, N - 1);
+      bfv[j] = *reinterpret_cast<const frag_t<T>*>(B2 + (size_t)r * 32 + fq * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(af[i], bfv[j], acc[i][j]);
+  }
+
+  // ---- epilogue phase 1: acc (*alpha, +bias) -> T tile in LDS [BM][BN] ----
+  T* Cs = reinterpret_cast<T*>(smem);
+  constexpr int CLD = BN + 8;  // padded row (elements) to spread banks
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wn * WN + j * 16 + fr;
+    float bv = 0.f;
+    if (ep.bias != nullptr && n0 + col < N)
+      bv = ep.bias_f32 ? reinterpret_cast<const float*>(ep.bias)[n0 + col]
+                       : (float)reinterpret_cast<const T*>(ep.bias)[n0 + col];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * WM + i * 16 + fq * 4 + e;
+        Cs[row * CLD + col] = (T)(acc[i][j][e] * ep.alpha + bv);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue phase 2: 8 columns per thread, 16-B vector I/O ----
+  constexpr int VPR = BN / 8;  // vectors per row
+  for (int v = tid; v < BM * VPR; v += 256) {
+    const int row = v / VPR, c8 = (v % VPR) * 8;
+    const int gr = m0 + row, gc = n0 + c8;
+    if (gr >= M || gc >= N) continue;
+    float z[8];
+    load8<T>(Cs + row * CLD + c8, z);
+    const size_t off = (size_t)gr * ldc + gc;
+    const bool full = gc + 8 <= N;
+    if (ep.preact != nullptr) {
+      if (full) store8<T>(reinterpret_cast<T*>(ep.preact) + off, z);
+      else for (int e = 0; e < N - gc; ++e) reinterpret_cast<T*>(ep.preact)[off + e] = (T)z[e];
+    }
+    if (ep.act != ACT_NONE) {
+      float ax[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (ep.aux != nullptr) {
+        if (full) load8<T>(reinterpret_cast<const T*>(ep.aux) + off, ax);
+        else for (int e = 0; e < N - gc; ++e) ax[e] = (float)reinterpret_cast<const T*>(ep.aux)[off + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = apply_act(ep.act, z[e], ax[e]);
+    }
+    if (ep.thr != 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        uint64_t idx = (uint64_t)gr * N + gc + e;
+        z[e] = mift_keep(ep.seed, idx, ep.thr) ? z[e] * ep.inv_keep : 0.f;
+      }
+    }
+    if (ep.residual != nullptr) {
+      float rv[8];
+      if (full) load8<T>(reinterpret_cast<const T*>(ep.residual) + off, rv);
+      else for (int e = 0; e < N - gc; ++e) rv[e] = (float)reinterpret_cast<const T*>(ep.residual)[off + e];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] += rv[e];
+    }
+    if (full) store8<T>(C + off, z);
+    else for (int e = 0; e < N - gc; ++e) C[off + e] = (T)z[e];
+  }
+}
+
+template <typename T, int BM, int BN>
+void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
+                 int K, const EpiArgs& ep, hipStream_t st) {
+  constexpr int STAGE_BYTES = (BM + BN) * ROWB;
+  constexpr int EPI_BYTES = BM * (BN + 8) * 2;
+  constexpr int SMEM = (2 * STAGE_BYTES > EPI_BYTES) ? 2 * STAGE_BYTES : EPI_BYTES;
+  const int nblk = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN>), dim3(nblk), dim3(256), SMEM, st, (const T*)a.data_ptr(),
+                     (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0),
+                     (int)b.stride(0), (int)c.stride(0), ep);
+}
+
+template <typename T>
+void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
+                   int K, const EpiArgs& ep, hipStream_t st, int tile) {
+  // tile: 0 = auto
+  if (tile == 0) {
+    const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+    tile = (t128 >= 512) ? 1 : 2;
+  }
+  if (tile == 1) launch_gemm<T, 128, 128>(a, b, c, a2, b2, M, N, K, ep, st);
+  else if (tile == 2) launch_gemm<T, 128, 64>(a, b, c, a2, b2, M, N, K, ep, st);
+  else launch_gemm<T, 64, 64>(a, b, c, a2, b2, M, N, K, ep, st);
+}
+
+}  // namespace
+
+// out = epi(a @ b^T [+ a2 @ b2^T]).  a:[M,K], b:[N,K] (K-contiguous, K%64==0).
+std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                        const c10::optional<at::Tensor>& a2, const c10::optional<at::Tensor>& b2, int64_t act,
+                        const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& residual,
+                        double dropout_p, int64_t seed, bool want_preact, double alpha,
+                        const c10::optional<at::Tensor>& out, int64_t tile) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm_nt: GPU tensors required");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_nt: 2-D operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_nt: K must be contiguous");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_nt: dtype mismatch");
+  const int M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm_nt: K mismatch");
+  TORCH_CHECK(K % 64 == 0, "gemm_nt: K must be a multiple of 64, got ", K);
+  TORCH_CHECK((a.stride(0) % 8) == 0 && (b.stride(0) % 8) == 0, "gemm_nt: row strides must be 16-B aligned");
+  at::Tensor c = out ? *out : at::empty({M, N}, a.options());
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.stride(0) % 8 == 0, "gemm_nt: bad out");
+  EpiArgs ep{};
+  ep.bias = nullptr;
+  if (bias) {
+    TORCH_CHECK(bias->numel() == N, "gemm_nt: bias size");
+    ep.bias = bias->data_ptr();
+    ep.bias_f32 = bias->scalar_type() == at::kFloat;
+  }
+  if (a2) {
+    TORCH_CHECK(b2.has_value(), "gemm_nt: a2 needs b2");
+    TORCH_CHECK(a2->size(0) == M && a2->size(1) == 32 && a2->is_contiguous(), "gemm_nt: a2 must be [M,32]");
+    TORCH_CHECK(b2->size(0) == N && b2->size(1) == 32 && b2->is_contiguous(), "gemm_nt: b2 must be [N,32]");
+  }
+  ep.act = (int)act;
+  ep.aux = nullptr;
+  if (aux) {
+    TORCH_CHECK(aux->size(0) == M && aux->size(1) == N && aux->stride(0) == c.stride(0) && aux->stride(1) == 1,
+                "gemm_nt: aux layout must match out");
+    ep.aux = aux->data_ptr();
+  }
+  at::Tensor pre;
+  ep.preact = nullptr;
+  if (want_preact) {
+    TORCH_CHECK(c.stride(0) == N, "gemm_nt: preact output needs a dense out");
+    pre = at::empty({M, N}, a.options());
+    ep.preact = pre.data_ptr();
+  }
+  ep.residual = nullptr;
+  if (residual) {
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N && residual->stride(0) == c.stride(0),
+                "gemm_nt: residual layout must match out");
+    ep.residual = residual->data_ptr();
+  }
+  ep.seed = (uint64_t)seed;
+  ep.thr = dropout_p > 0 ? (uint32_t)std::min(4294967295.0, dropout_p * 4294967296.0) : 0u;
+  ep.inv_keep = dropout_p > 0 ? (float)(1.0 / (1.0 - dropout_p)) : 1.f;
+  ep.alpha = (float)alpha;
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  if (a.scalar_type() == at::kBFloat16) {
+    dispatch_tile<bf16>(a, b, c, a2 ? (const bf16*)a2->data_ptr() : nullptr, b2 ? (const bf16*)b2->data_ptr() : nullptr,
+                        M, N, K, ep, st, (int)tile);
+  } else if (a.scalar_type() == at::kHalf) {
+    dispatch_tile<fp16>(a, b, c, a2 ? (const fp16*)a2->data_ptr() : nullptr, b2 ? (const fp16*)b2->data_ptr() : nullptr,
+                        M, N, K, ep, st, (int)tile);
+  } else {
+    TORCH_CHECK(false, "gemm_nt: bf16/fp16 only");
+  }
+  return {c, pre};
+}

@@ -1,0 +1,280 @@
+// K4: LayerNorm forward / backward (GPT-2 ln_1/ln_2/ln_f, OPT pre-LN,
+// BERT post-LN).  Reference op: HF nn.LayerNorm (eps 1e-5 GPT-2/OPT,
+// 1e-12 BERT) — see SURVEY §2.4 K4.
+//
+// Mapping: one wave per row, 4 rows per 256-thread block, the row held in
+// registers (VEC=4 elements per lane per pass, NIT passes), so x is read
+// exactly once from HBM.  Statistics in fp32 (two-pass mean/var on the
+// register copy: no E[x^2]-E[x]^2 cancellation).
+//
+// Backward fuses (a) the residual-stream gradient add (dx += dres) and
+// (b) the dropout-masked copy for the parallel branch of a pre-LN block
+// (dbranch = keep(seed, idx) * dx / (1-p)), so the block backward reads the
+// residual gradient once instead of three times.
+#include "common.h"
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+namespace {
+
+constexpr int VEC = 4;
+
+template <typename T>
+MIFT_HD void ld4(const T* p, float* o) {
+  if constexpr (sizeof(T) == 4) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  } else {
+    short4_ v = *reinterpret_cast<const short4_*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { short s = v[i]; T t; __builtin_memcpy(&t, &s, 2); o[i] = (float)t; }
+  }
+}
+template <typename T>
+MIFT_HD void st4(T* p, const float* o) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  } else {
+    short4_ v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { T t = (T)o[i]; short s; __builtin_memcpy(&s, &t, 2); v[i] = s; }
+    *reinterpret_cast<short4_*>(p) = v;
+  }
+}
+
+template <typename T, typename W, int NIT>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const W* __restrict__ w,
+                                                     const W* __restrict__ b, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const T* xr = x + (size_t)row * D;
+  float v[NIT][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    int c = (it * 64 + lane) * VEC;
+    if (c < D) {
+      ld4(xr + c, v[it]);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) s += v[it][i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) v[it][i] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    int c = (it * 64 + lane) * VEC;
+    if (c < D) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) { float d = v[it][i] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / D + eps);
+  T* yr = y + (size_t)row * D;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    int c = (it * 64 + lane) * VEC;
+    if (c < D) {
+      float wv[VEC], bv[VEC], o[VEC];
+      ld4(w + c, wv);
+      ld4(b + c, bv);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) o[i] = (v[it][i] - mean) * rstd * wv[i] + bv[i];
+      st4(yr + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
+template <typename T, typename W, int NIT>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const T* __restrict__ dres,
+                                                     T* __restrict__ dx, T* __restrict__ dbranch,
+                                                     float* __restrict__ dw, float* __restrict__ db, int M, int D,
+                                                     uint64_t seed, uint32_t thr, float inv_keep) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  const T* xr = x + (size_t)row * D;
+  const T* dyr = dy + (size_t)row * D;
+  float xh[NIT][VEC], g[NIT][VEC];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    int c = (it * 64 + lane) * VEC;
+    if (c < D) {
+      float xv[VEC], dv[VEC], wv[VEC];
+      ld4(xr + c, xv);
+      ld4(dyr + c, dv);
+      ld4(w + c, wv);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        xh[it][i] = (xv[i] - mean) * rstd;
+        g[it][i] = dv[i] * wv[i];
+        sg += g[it][i];
+        sgx += g[it][i] * xh[it][i];
+      }
+      if (dw != nullptr) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          atomicAdd(dw + c + i, dv[i] * xh[it][i]);
+          atomicAdd(db + c + i, dv[i]);
+        }
+      }
+    }
+  }
+  sg = wave_sum(sg) / D;
+  sgx = wave_sum(sgx) / D;
+  T* dxr = dx + (size_t)row * D;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    int c = (it * 64 + lane) * VEC;
+    if (c < D) {
+      float o[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) o[i] = rstd * (g[it][i] - sg - xh[it][i] * sgx);
+      if (dres != nullptr) {
+        float r[VEC];
+        ld4(dres + (size_t)row * D + c, r);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) o[i] += r[i];
+      }
+      st4(dxr + c, o);
+      if (dbranch != nullptr) {
+        float m[VEC];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          uint64_t idx = (uint64_t)row * D + c + i;
+          m[i] = mift_keep(seed, idx, thr) ? o[i] * inv_keep : 0.f;
+        }
+        st4(dbranch + (size_t)row * D + c, m);
+      }
+    }
+  }
+}
+
+template <typename T, typename W, int N>
+void ln_fwd_launch(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Tensor& y, at::Tensor& mean,
+                   at::Tensor& rstd, int M, int D, float eps, hipStream_t st) {
+  dim3 grid((M + 3) / 4), block(256);
+  ln_fwd_kernel<T, W, N><<<grid, block, 0, st>>>((const T*)x.data_ptr(), (const W*)w.data_ptr(),
+                                                 (const W*)b.data_ptr(), (T*)y.data_ptr(), mean.data_ptr<float>(),
+                                                 rstd.data_ptr<float>(), M, D, eps);
+}
+
+template <typename T, typename W>
+void launch_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Tensor& y, at::Tensor& mean,
+                at::Tensor& rstd, int M, int D, float eps, hipStream_t st) {
+  int nit = (D + 255) / 256;
+  if (nit <= 1) ln_fwd_launch<T, W, 1>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 2) ln_fwd_launch<T, W, 2>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 3) ln_fwd_launch<T, W, 3>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 4) ln_fwd_launch<T, W, 4>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 6) ln_fwd_launch<T, W, 6>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 8) ln_fwd_launch<T, W, 8>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 10) ln_fwd_launch<T, W, 10>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 12) ln_fwd_launch<T, W, 12>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 16) ln_fwd_launch<T, W, 16>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else if (nit <= 32) ln_fwd_launch<T, W, 32>(x, w, b, y, mean, rstd, M, D, eps, st);
+  else TORCH_CHECK(false, "layer_norm: hidden size too large: ", D);
+}
+
+template <typename T, typename W, int N>
+void ln_bwd_launch(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& mean,
+                   const at::Tensor& rstd, const c10::optional<at::Tensor>& dres, at::Tensor& dx,
+                   const c10::optional<at::Tensor>& dbranch, const c10::optional<at::Tensor>& dw,
+                   const c10::optional<at::Tensor>& db, int M, int D, uint64_t seed, uint32_t thr, float inv_keep,
+                   hipStream_t st) {
+  dim3 grid((M + 3) / 4), block(256);
+  ln_bwd_kernel<T, W, N><<<grid, block, 0, st>>>(
+      (const T*)dy.data_ptr(), (const T*)x.data_ptr(), (const W*)w.data_ptr(), mean.data_ptr<float>(),
+      rstd.data_ptr<float>(), dres ? (const T*)dres->data_ptr() : nullptr, (T*)dx.data_ptr(),
+      dbranch ? (T*)dbranch->data_ptr() : nullptr, dw ? dw->data_ptr<float>() : nullptr,
+      db ? db->data_ptr<float>() : nullptr, M, D, seed, thr, inv_keep);
+}
+
+template <typename T, typename W>
+void launch_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& mean,
+                const at::Tensor& rstd, const c10::optional<at::Tensor>& dres, at::Tensor& dx,
+                const c10::optional<at::Tensor>& dbranch, const c10::optional<at::Tensor>& dw,
+                const c10::optional<at::Tensor>& db, int M, int D, uint64_t seed, uint32_t thr, float inv_keep,
+                hipStream_t st) {
+  int nit = (D + 255) / 256;
+  if (nit <= 1) ln_bwd_launch<T, W, 1>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 2) ln_bwd_launch<T, W, 2>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 3) ln_bwd_launch<T, W, 3>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 4) ln_bwd_launch<T, W, 4>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 6) ln_bwd_launch<T, W, 6>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 8) ln_bwd_launch<T, W, 8>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 10) ln_bwd_launch<T, W, 10>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 12) ln_bwd_launch<T, W, 12>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 16) ln_bwd_launch<T, W, 16>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else if (nit <= 32) ln_bwd_launch<T, W, 32>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
+  else TORCH_CHECK(false, "layer_norm_bwd: hidden size too large: ", D);
+}
+
+}  // namespace
+
+#define DISPATCH_TW(xdt, wdt, ...)                                                                   \
+  do {                                                                                               \
+    if (xdt == at::kBFloat16 && wdt == at::kBFloat16) { using T = bf16; using W = bf16; __VA_ARGS__; } \
+    else if (xdt == at::kBFloat16 && wdt == at::kFloat) { using T = bf16; using W = float; __VA_ARGS__; } \
+    else if (xdt == at::kHalf && wdt == at::kHalf) { using T = fp16; using W = fp16; __VA_ARGS__; }   \
+    else if (xdt == at::kHalf && wdt == at::kFloat) { using T = fp16; using W = float; __VA_ARGS__; }  \
+    else if (xdt == at::kFloat && wdt == at::kFloat) { using T = float; using W = float; __VA_ARGS__; } \
+    else TORCH_CHECK(false, "layer_norm: unsupported dtypes ", xdt, " / ", wdt);                  \
+  } while (0)
+
+std::vector<at::Tensor> mift_layer_norm_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
+                                            double eps) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "layer_norm: x must be contiguous GPU");
+  const int D = x.size(-1);
+  const int M = x.numel() / D;
+  TORCH_CHECK(D % 4 == 0, "layer_norm: D must be a multiple of 4");
+  TORCH_CHECK(w.numel() == D && b.numel() == D, "layer_norm: weight/bias size");
+  auto y = at::empty_like(x);
+  auto mean = at::empty({M}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  DISPATCH_TW(x.scalar_type(), w.scalar_type(), launch_fwd<T, W>(x, w, b, y, mean, rstd, M, D, (float)eps, st));
+  return {y, mean, rstd};
+}
+
+std::vector<at::Tensor> mift_layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                            const at::Tensor& mean, const at::Tensor& rstd,
+                                            const c10::optional<at::Tensor>& dres, bool want_branch, double p,
+                                            int64_t seed, bool want_wgrad) {
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "layer_norm_bwd: contiguous inputs");
+  const int D = x.size(-1);
+  const int M = x.numel() / D;
+  auto dx = at::empty_like(x);
+  c10::optional<at::Tensor> dbranch, dw, db;
+  if (want_branch) dbranch = at::empty_like(x);
+  if (want_wgrad) {
+    dw = at::zeros({D}, x.options().dtype(at::kFloat));
+    db = at::zeros({D}, x.options().dtype(at::kFloat));
+  }
+  uint32_t thr = (uint32_t)std::min(4294967295.0, p * 4294967296.0);
+  float inv_keep = p < 1.0 ? (float)(1.0 / (1.0 - p)) : 0.f;
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  DISPATCH_TW(x.scalar_type(), w.scalar_type(),
+              launch_bwd<T, W>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, (uint64_t)seed, thr,
+                               inv_keep, st));
+  std::vector<at::Tensor> out{dx};
+  out.push_back(want_branch ? *dbranch : at::Tensor());
+  out.push_back(want_wgrad ? *dw : at::Tensor());
+  out.push_back(want_wgrad ? *db : at::Tensor());
+  return out;
+}

@@ -1,0 +1,216 @@
+"""GPT-2 family (distilgpt2 = 6 layers) causal LM.
+
+Architecture parity: HF ``GPT2LMHeadModel`` as used by the reference
+(`Cluster/Project 1 - Fine Tuning Distilgpt2/finetune_lora_distilgpt2.py:80-92`,
+spec in README.md:52-61 / SURVEY Appendix C): pre-LN blocks, fused qkv
+``c_attn`` (Conv1D [in,out]), ``gelu_new`` MLP, learned positions, dropout
+0.1 (embd/attn/resid), LN eps 1e-5, LM head tied to ``wte``.
+
+Two execution paths over the same parameters:
+  * reference path (this file) — plain torch autograd, any device; the
+    CPU/gloo plumbing configuration and the numerics oracle;
+  * fused HIP path (``mift.models.gpt2_fused``) — block-level autograd
+    Functions over the gfx950 kernels; used for GPU tensors.
+"""
+from dataclasses import dataclass, asdict
+
+import torch
+import torch.nn as nn
+
+from ..ops import reference as ref
+from ..ops.dispatch import use_kernels
+from .layers import Embedding, LayerNorm, Linear, init_normal_, padded_vocab, seed_for
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_embd: int = 768
+    n_layer: int = 6
+    n_head: int = 12
+    n_inner: int = 3072
+    layer_norm_epsilon: float = 1e-5
+    embd_pdrop: float = 0.1
+    attn_pdrop: float = 0.1
+    resid_pdrop: float = 0.1
+    initializer_range: float = 0.02
+    bos_token_id: int = 50256
+    eos_token_id: int = 50256
+    pad_token_id: int = 50256
+    model_type: str = "gpt2"
+
+    @staticmethod
+    def preset(name: str) -> "GPT2Config":
+        name = name.split("/")[-1].lower()
+        if name in ("distilgpt2", "distilgpt2-lora"):
+            return GPT2Config(n_layer=6)
+        if name == "gpt2":
+            return GPT2Config(n_layer=12)
+        if name == "gpt2-medium":
+            return GPT2Config(n_layer=24, n_embd=1024, n_head=16, n_inner=4096)
+        if name in ("gpt2-tiny", "tiny-gpt2"):
+            return GPT2Config(n_layer=2, n_embd=64, n_head=2, n_inner=256, vocab_size=1000, n_positions=128)
+        raise ValueError(f"unknown GPT-2 preset {name}")
+
+    def to_hf_dict(self):
+        d = asdict(self)
+        d.update({"architectures": ["GPT2LMHeadModel"], "activation_function": "gelu_new",
+                  "n_ctx": self.n_positions, "tie_word_embeddings": True})
+        return d
+
+
+class GPT2Attention(nn.Module):
+    def __init__(self, cfg: GPT2Config, dtype=None, device=None):
+        super().__init__()
+        self.n_head = cfg.n_head
+        self.head_dim = cfg.n_embd // cfg.n_head
+        self.c_attn = Linear(cfg.n_embd, 3 * cfg.n_embd, conv1d=True, dtype=dtype, device=device)
+        self.c_proj = Linear(cfg.n_embd, cfg.n_embd, conv1d=True, dtype=dtype, device=device)
+
+
+class GPT2MLP(nn.Module):
+    def __init__(self, cfg: GPT2Config, dtype=None, device=None):
+        super().__init__()
+        self.c_fc = Linear(cfg.n_embd, cfg.n_inner, conv1d=True, dtype=dtype, device=device)
+        self.c_proj = Linear(cfg.n_inner, cfg.n_embd, conv1d=True, dtype=dtype, device=device)
+
+
+class GPT2Block(nn.Module):
+    def __init__(self, cfg: GPT2Config, idx: int, dtype=None, device=None):
+        super().__init__()
+        self.idx = idx
+        self.cfg = cfg
+        self.ln_1 = LayerNorm(cfg.n_embd, cfg.layer_norm_epsilon, dtype=dtype, device=device)
+        self.attn = GPT2Attention(cfg, dtype, device)
+        self.ln_2 = LayerNorm(cfg.n_embd, cfg.layer_norm_epsilon, dtype=dtype, device=device)
+        self.mlp = GPT2MLP(cfg, dtype, device)
+
+    def site_seeds(self, base, step):
+        s = 100 + 10 * self.idx
+        return {k: seed_for(base, step, s + i) for i, k in
+                enumerate(["attn", "attn_out", "mlp_out", "lora_attn", "lora_proj", "lora_mlp"])}
+
+    def forward_ref(self, h, seeds, training, key_valid=None):
+        """h: [B, S, d] (reference path)."""
+        B, S, d = h.shape
+        H, hd = self.attn.n_head, self.attn.head_dim
+        cfg = self.cfg
+        a = self.ln_1(h)
+        qkv = self.attn.c_attn(a, seeds["lora_attn"])
+        q, k, v = qkv.split(d, dim=-1)
+        q = q.view(B, S, H, hd).transpose(1, 2)
+        k = k.view(B, S, H, hd).transpose(1, 2)
+        v = v.view(B, S, H, hd).transpose(1, 2)
+        o = ref.attention(q, k, v, causal=True, key_padding=key_valid, scale=hd ** -0.5,
+                          dropout_p=cfg.attn_pdrop if training else 0.0, seed=seeds["attn"])
+        o = o.transpose(1, 2).reshape(B, S, d)
+        y = self.attn.c_proj(o, seeds["lora_proj"])
+        if training and cfg.resid_pdrop > 0:
+            y = ref.dropout(y, cfg.resid_pdrop, seeds["attn_out"])
+        h = h + y
+        a2 = self.ln_2(h)
+        f = ref.gelu_new(self.mlp.c_fc(a2))
+        y2 = self.mlp.c_proj(f, seeds["lora_mlp"])
+        if training and cfg.resid_pdrop > 0:
+            y2 = ref.dropout(y2, cfg.resid_pdrop, seeds["mlp_out"])
+        return h + y2
+
+
+class GPT2LMHeadModel(nn.Module):
+    """HF-compatible GPT-2 LM.  ``forward(input_ids, attention_mask, labels)``."""
+
+    def __init__(self, cfg: GPT2Config, dtype=torch.float32, device=None, layer_range=None,
+                 has_embed=True, has_head=True):
+        super().__init__()
+        self.config = cfg
+        self.dtype_ = dtype
+        n = cfg.n_layer
+        self.layer_range = layer_range or (0, n)
+        self.has_embed, self.has_head = has_embed, has_head
+        self.vocab_padded = padded_vocab(cfg.vocab_size)
+        self.transformer = nn.Module()
+        if has_embed or has_head:
+            self.transformer.wte = Embedding(cfg.vocab_size, cfg.n_embd, dtype=dtype, device=device)
+        if has_embed:
+            self.transformer.wpe = Embedding(cfg.n_positions, cfg.n_embd, dtype=dtype, device=device)
+        self.transformer.h = nn.ModuleList(
+            [GPT2Block(cfg, i, dtype, device) if self.layer_range[0] <= i < self.layer_range[1] else nn.Identity()
+             for i in range(n)])
+        if has_head:
+            self.transformer.ln_f = LayerNorm(cfg.n_embd, cfg.layer_norm_epsilon, dtype=dtype, device=device)
+        self.seed = 0
+        self.micro_step = 0
+        self.fused = True  # use HIP kernels for GPU tensors
+        self.recompute = False
+        self._head_cache = None
+
+    # ---- init / misc ----
+    def init_weights(self, seed=0):
+        g = torch.random.fork_rng(devices=[])
+        with g:
+            torch.manual_seed(seed)
+            std = self.config.initializer_range
+            init_normal_(self, std, proj_std=std / (2 * self.config.n_layer) ** 0.5)
+        return self
+
+    def blocks(self):
+        return [b for b in self.transformer.h if isinstance(b, GPT2Block)]
+
+    def lm_weight_padded(self):
+        """Tied LM head as [V_pad, d] (zero rows beyond vocab) for the HIP GEMM."""
+        w = self.transformer.wte.weight
+        key = (w.data_ptr(), w.dtype, w.device)
+        if self._head_cache is None or self._head_cache[0] != key:
+            wp = torch.zeros(self.vocab_padded, w.shape[1], dtype=w.dtype, device=w.device)
+            wp[: w.shape[0]].copy_(w.detach())
+            self._head_cache = (key, wp, wp.t().contiguous())
+        return self._head_cache[1], self._head_cache[2]
+
+    def next_micro_step(self):
+        self.micro_step += 1
+
+    def embed_seed(self):
+        return seed_for(self.seed, self.micro_step, 1)
+
+    # ---- reference path pieces ----
+    def embed_ref(self, input_ids, attention_mask=None):
+        B, S = input_ids.shape
+        pos = torch.arange(S, device=input_ids.device)
+        h = self.transformer.wte(input_ids) + self.transformer.wpe(pos)[None]
+        if self.training and self.config.embd_pdrop > 0:
+            h = ref.dropout(h, self.config.embd_pdrop, self.embed_seed())
+        return h
+
+    def head_ref(self, h, labels, reduction="mean"):
+        h = self.transformer.ln_f(h)
+        logits = h @ self.transformer.wte.weight.t()
+        if labels is None:
+            return None, logits
+        sl = logits[:, :-1].reshape(-1, logits.shape[-1])
+        tl = labels[:, 1:].reshape(-1)
+        loss = torch.nn.functional.cross_entropy(sl.float(), tl, ignore_index=-100, reduction=reduction)
+        return loss, logits
+
+    def _use_fused(self, t):
+        return self.fused and use_kernels(t)
+
+    def forward(self, input_ids=None, attention_mask=None, labels=None, hidden_states=None, reduction="mean",
+                return_logits=True):
+        ref_in = input_ids if input_ids is not None else hidden_states
+        if self._use_fused(ref_in):
+            from .gpt2_fused import fused_forward
+            return fused_forward(self, input_ids, attention_mask, labels, hidden_states, reduction, return_logits)
+        key_valid = None
+        h = self.embed_ref(input_ids, attention_mask) if self.has_embed else hidden_states
+        for blk in self.blocks():
+            seeds = blk.site_seeds(self.seed, self.micro_step)
+            if self.recompute and self.training:
+                h = torch.utils.checkpoint.checkpoint(blk.forward_ref, h, seeds, self.training, key_valid,
+                                                      use_reentrant=False)
+            else:
+                h = blk.forward_ref(h, seeds, self.training, key_valid)
+        if not self.has_head:
+            return {"hidden_states": h}
+        loss, logits = self.head_ref(h, labels, reduction)
+        return {"loss": loss, "logits": logits if return_logits else None}
