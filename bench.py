@@ -1,0 +1,141 @@
+#!/usr/bin/env python
+"""Flagship benchmark: distilgpt2 LoRA DDP fine-tuning throughput on MI355X.
+
+Metric/config from BASELINE.json config #2: distilgpt2 LoRA (r=8, alpha=16,
+dropout 0.05, targets c_attn,c_proj), bf16, seq_len 256, per-rank effective
+batch 32 (reference batch 1 x accum 32, run as 32 x 1 — identical
+token-normalised update), AdamW + clip 1.0 + linear LR, synthetic
+OpenWebText-shaped tokens, random-init weights (no network).  One "step" =
+one full optimizer step (forward, backward, gradient all-reduce over RCCL,
+fused AdamW).  Weak scaling: every rank processes 32 x 256 tokens per step.
+
+  python bench.py --gpus N --steps K --warmup W
+  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Prints ONE JSON line on rank 0.  `value` = whole-job tokens/s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="distilgpt2")
+    ap.add_argument("--seq_len", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--accum", type=int, default=32)
+    ap.add_argument("--fold_accum", type=int, default=1)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
+                    help="fused = mift HIP kernels; torch = eager PyTorch ops on the same model (comparison)")
+    ap.add_argument("--profile_dir", default=None, help="torch.profiler chrome trace of 3 steps")
+    a = ap.parse_args()
+
+    if a.impl == "torch":
+        os.environ["MIFT_KERNELS"] = "0"
+    import torch
+    import torch.distributed as dist
+
+    import mift
+    from mift import lora as L
+    from mift.data import MicroBatcher, synthetic_openwebtext
+    from mift.models import build_causal_lm
+    from mift.parallel import dist as D
+    from mift.train.trainer import TrainConfig, Trainer
+
+    ctx = D.init(verbose=False, sanity=True)
+    if a.gpus != ctx.world:
+        if ctx.rank == 0:
+            print(f"warning: --gpus {a.gpus} != WORLD_SIZE {ctx.world}; using WORLD_SIZE", file=sys.stderr)
+    n = ctx.world
+    assert ctx.device.type == "cuda", "bench.py needs a GPU"
+    if a.impl == "fused":
+        assert mift.kernels_available(), f"HIP extension not loaded: {mift._ext.error()!r}"
+    dtype = torch.bfloat16 if a.precision == "bf16" else torch.float16
+
+    model = build_causal_lm(a.model, dtype=dtype, device=ctx.device, seed=0)
+    L.inject(model, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["c_attn", "c_proj"],
+                                 base_model_name_or_path=a.model))
+    if a.impl == "torch":
+        model.fused = False
+    per_rank = a.batch * a.accum
+    mb, acc = (per_rank, 1) if a.fold_accum else (a.batch, a.accum)
+    total_steps = a.warmup + a.steps
+    ds = synthetic_openwebtext(per_rank * n * total_steps, a.seq_len, model.config.vocab_size,
+                               model.config.pad_token_id, seed=1234, full_length=True)
+    batcher = MicroBatcher(ds, mb, acc, rank=ctx.dp_rank, world=ctx.dp)
+    tr = Trainer(model, batcher, TrainConfig(epochs=1, batch=mb, accum=acc, lr=5e-5, precision=a.precision,
+                                             logging_steps=0, save_steps=0, step_log="none"), ctx)
+    model.train()
+    steps = list(batcher.epoch(0))
+    assert len(steps) >= total_steps
+
+    def run(i):
+        tr.train_step(steps[i])
+
+    for i in range(a.warmup):
+        run(i)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.warmup, total_steps):
+        run(i)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
+    if dist.is_initialized() and n > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item()
+    ms = dt / a.steps * 1000.0
+    tokens_per_step = per_rank * a.seq_len * n
+    value = tokens_per_step / (ms / 1000.0)
+    stats = tr.opt.stats()
+    if a.profile_dir and ctx.rank == 0:
+        from torch.profiler import profile, ProfilerActivity
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for i in range(min(3, len(steps))):
+                run(i % len(steps))
+            torch.cuda.synchronize()
+        os.makedirs(a.profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
+        with open(os.path.join(a.profile_dir, "table.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
+    if ctx.rank == 0:
+        out = {
+            "metric": "distilgpt2 LoRA DDP fine-tune throughput (tokens/sec, whole job)",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.precision,
+            "data": "synthetic (OpenWebText-shaped random tokens, full 256-token lines); random-init weights",
+            "config": {"model": a.model, "global_batch": per_rank * n, "seq_len": a.seq_len,
+                       "parallelism": f"dp{n}", "per_rank_batch": f"{a.batch}x{a.accum}",
+                       "lora": "r8/a16/p0.05 c_attn,c_proj", "impl": a.impl,
+                       "tokens_per_gpu_per_s": round(value / n, 1),
+                       "final_grad_norm": round(stats["grad_norm"], 4)},
+        }
+        print(json.dumps(out), flush=True)
+    D.destroy()
+
+
+if __name__ == "__main__":
+    main()

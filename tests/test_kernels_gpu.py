@@ -44,7 +44,7 @@ def test_gemm_nt_plain(M, N, K):
     torch.manual_seed(1)
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
-    out = C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0)[0]
+    out = C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None)[0]
     exp = a.float() @ b.float().t()
     torch.testing.assert_close(out.float(), exp, atol=3e-2, rtol=2e-2)
 
@@ -55,7 +55,7 @@ def test_gemm_nt_identity_asymmetric():
     n = 128
     a = torch.eye(n, device="cuda", dtype=torch.bfloat16)
     bm = (torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
-    out = C.gemm_nt(a, bm, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0)[0]
+    out = C.gemm_nt(a, bm, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None)[0]
     torch.testing.assert_close(out.float(), bm.float().t())
 
 
@@ -70,7 +70,7 @@ def test_gemm_nt_fused_epilogue(act):
     a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
     b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
     res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-    out, pre = C.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True, 1.0, None, 0)
+    out, pre = C.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True, 1.0, None, 0, None, None)
     exp, exp_pre = ref.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True)
     torch.testing.assert_close(pre.float(), exp_pre.float(), atol=5e-2, rtol=2e-2)
     torch.testing.assert_close(out.float(), exp.float(), atol=8e-2, rtol=3e-2)
@@ -84,6 +84,59 @@ def test_gemm_nt_act_backward(act):
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
     aux = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-    out = C.gemm_nt(a, b, None, None, None, act, aux, None, 0.0, 0, False, 1.0, None, 0)[0]
+    out = C.gemm_nt(a, b, None, None, None, act, aux, None, 0.0, 0, False, 1.0, None, 0, None, None)[0]
     exp, _ = ref.gemm_nt(a, b, None, None, None, act, aux)
     torch.testing.assert_close(out.float(), exp.float(), atol=5e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("V,ldV", [(1000, 1024), (50257, 50304)])
+def test_xent_fwd_bwd(V, ldV):
+    C = _C()
+    torch.manual_seed(4)
+    M = 64
+    logits = (torch.randn(M, ldV, device="cuda") * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (M,), device="cuda")
+    labels[::7] = -100
+    x = logits[:, :V].float().requires_grad_(True)
+    ref_loss = torch.nn.functional.cross_entropy(x, labels, ignore_index=-100, reduction="none")
+    ref_loss.sum().backward()
+    buf = logits.clone()
+    loss, lse = C.xent_fwd_bwd(buf, labels, V, -100, True)
+    torch.testing.assert_close(loss, ref_loss.detach(), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(buf[:, :V].float(), x.grad, atol=1e-2, rtol=2e-2)
+    assert (buf[:, V:] == 0).all()
+
+
+def test_adamw_matches_torch():
+    C = _C()
+    torch.manual_seed(5)
+    n = 10_000
+    p = torch.randn(n, device="cuda")
+    g = torch.randn(n, device="cuda") * 3.0
+    from mift.train.optim import FusedAdamW
+    pt = p.clone().requires_grad_(True)
+    ref = torch.optim.AdamW([pt], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    opt = FusedAdamW(p, g.clone(), lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
+    for _ in range(3):
+        gg = g.clone()
+        opt.g.copy_(gg)
+        opt.step()
+        pt.grad = gg.clone()
+        torch.nn.utils.clip_grad_norm_([pt], 1.0)
+        ref.step()
+    torch.testing.assert_close(opt.p, pt.detach(), atol=1e-5, rtol=1e-4)
+    assert opt.g.abs().max().item() == 0.0
+
+
+def test_mask_scale_and_embed():
+    C = _C()
+    x = torch.randn(1000, 64, device="cuda", dtype=torch.bfloat16)
+    y = C.mask_scale(x, 0.1, 99, None, False)
+    exp = ref.dropout(x.float(), 0.1, 99)
+    torch.testing.assert_close(y.float(), exp, atol=1e-2, rtol=1e-2)
+    wte = torch.randn(500, 64, device="cuda", dtype=torch.bfloat16)
+    wpe = torch.randn(128, 64, device="cuda", dtype=torch.bfloat16)
+    ids = torch.randint(0, 500, (4, 32), device="cuda")
+    h = C.embed_fwd(ids, None, wte, wpe, 0, 0.0, 0, torch.bfloat16)
+    e = (wte[ids].float() + wpe[torch.arange(32, device="cuda")][None].float()).view(-1, 64)
+    torch.testing.assert_close(h.float(), e, atol=2e-2, rtol=1e-2)

@@ -85,29 +85,41 @@ MIFT_HD float block_sum(float v, float* scratch) {
   return r;
 }
 
-// Vector load/store of 8 16-bit elements (16 B per lane, Guideline 13).
+// Vector load/store of 8 elements (16 B per lane for 16-bit types, Guideline 13).
 template <typename T>
 MIFT_HD void load8(const T* p, float* out) {
-  short8 v = *reinterpret_cast<const short8*>(p);
+  if constexpr (sizeof(T) == 4) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+    out[4] = b.x; out[5] = b.y; out[6] = b.z; out[7] = b.w;
+  } else {
+    short8 v = *reinterpret_cast<const short8*>(p);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    short s = v[i];
-    T t;
-    __builtin_memcpy(&t, &s, 2);
-    out[i] = (float)t;
+    for (int i = 0; i < 8; ++i) {
+      short s = v[i];
+      T t;
+      __builtin_memcpy(&t, &s, 2);
+      out[i] = (float)t;
+    }
   }
 }
 template <typename T>
 MIFT_HD void store8(T* p, const float* in) {
-  short8 v;
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(in[0], in[1], in[2], in[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(in[4], in[5], in[6], in[7]);
+  } else {
+    short8 v;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    T t = (T)in[i];
-    short s;
-    __builtin_memcpy(&s, &t, 2);
-    v[i] = s;
+    for (int i = 0; i < 8; ++i) {
+      T t = (T)in[i];
+      short s;
+      __builtin_memcpy(&s, &t, 2);
+      v[i] = s;
+    }
+    *reinterpret_cast<short8*>(p) = v;
   }
-  *reinterpret_cast<short8*>(p) = v;
 }
 
 #define MIFT_CHECK_HIP(expr)                                                        \

@@ -58,6 +58,8 @@ struct EpiArgs {
   uint32_t thr;      // dropout threshold (0 = no dropout)
   float inv_keep;
   float alpha;       // acc scale
+  const float* alpha_ptr;  // optional device-side extra scale (e.g. upstream grad / loss scale)
+  const void* pre_add;     // [M,N] T added to z before the activation
 };
 
 template <typename T>
@@ -204,6 +206,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
   // ---- epilogue phase 1: acc (*alpha, +bias) -> T tile in LDS [BM][BN] ----
   T* Cs = reinterpret_cast<T*>(smem);
   constexpr int CLD = BN + 8;  // padded row (elements) to spread banks
+  const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = wn * WN + j * 16 + fr;
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = wm * WM + i * 16 + fq * 4 + e;
-        Cs[row * CLD + col] = (T)(acc[i][j][e] * ep.alpha + bv);
+        Cs[row * CLD + col] = (T)(acc[i][j][e] * alpha + bv);
       }
     }
   }
@@ -232,6 +235,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
     load8<T>(Cs + row * CLD + c8, z);
     const size_t off = (size_t)gr * ldc + gc;
     const bool full = gc + 8 <= N;
+    if (ep.pre_add != nullptr) {
+      float pa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (full) load8<T>(reinterpret_cast<const T*>(ep.pre_add) + off, pa);
+      else for (int e = 0; e < N - gc; ++e) pa[e] = (float)reinterpret_cast<const T*>(ep.pre_add)[off + e];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] += pa[e];
+    }
     if (ep.preact != nullptr) {
       if (full) store8<T>(reinterpret_cast<T*>(ep.preact) + off, z);
       else for (int e = 0; e < N - gc; ++e) reinterpret_cast<T*>(ep.preact)[off + e] = (T)z[e];
@@ -296,7 +306,8 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                         const c10::optional<at::Tensor>& a2, const c10::optional<at::Tensor>& b2, int64_t act,
                         const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& residual,
                         double dropout_p, int64_t seed, bool want_preact, double alpha,
-                        const c10::optional<at::Tensor>& out, int64_t tile) {
+                        const c10::optional<at::Tensor>& out, int64_t tile,
+                        const c10::optional<at::Tensor>& alpha_t, const c10::optional<at::Tensor>& pre_add) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm_nt: GPU tensors required");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_nt: 2-D operands");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_nt: K must be contiguous");
@@ -343,6 +354,18 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
   ep.thr = dropout_p > 0 ? (uint32_t)std::min(4294967295.0, dropout_p * 4294967296.0) : 0u;
   ep.inv_keep = dropout_p > 0 ? (float)(1.0 / (1.0 - dropout_p)) : 1.f;
   ep.alpha = (float)alpha;
+  ep.alpha_ptr = nullptr;
+  if (alpha_t) {
+    TORCH_CHECK(alpha_t->scalar_type() == at::kFloat && alpha_t->is_cuda(), "gemm_nt: alpha_t fp32 GPU");
+    ep.alpha_ptr = alpha_t->data_ptr<float>();
+  }
+  ep.pre_add = nullptr;
+  if (pre_add) {
+    TORCH_CHECK(pre_add->size(0) == M && pre_add->size(1) == N && pre_add->stride(0) == c.stride(0) &&
+                    pre_add->scalar_type() == a.scalar_type(),
+                "gemm_nt: pre_add layout must match out");
+    ep.pre_add = pre_add->data_ptr();
+  }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   if (a.scalar_type() == at::kBFloat16) {
     dispatch_tile<bf16>(a, b, c, a2 ? (const bf16*)a2->data_ptr() : nullptr, b2 ? (const bf16*)b2->data_ptr() : nullptr,

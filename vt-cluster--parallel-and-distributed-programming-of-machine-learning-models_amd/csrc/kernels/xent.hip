@@ -1,0 +1,125 @@
+// K7: causal-LM cross-entropy over [M, V] logits with the gradient produced
+// in the same launch (the loss is the graph's last node, so dL/dlogits is
+// known at forward time).
+//
+// One 256-thread block per row: pass 1 = online (max, sum-exp) over the row
+// with 16-B loads; pass 2 = overwrite the row in place with
+// softmax - onehot(label) (unscaled; the LM-head dgrad GEMM applies the
+// upstream gradient / loss scale through its device-side alpha).  Rows
+// whose label == ignore_index get loss 0 and a zero gradient row; padded
+// vocabulary columns [V, ldV) are written as zeros so the dgrad GEMM over
+// the padded K dimension is exact.
+// Reference semantics: HF shifted CE with ignore_index=-100 (GPT-2) /
+// pad id (OPT OPTHead, P2/finetune_lora_opt_pp.py:143-152).
+#include "common.h"
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void xent_kernel(T* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                   float* __restrict__ loss, float* __restrict__ lse_out, int V,
+                                                   int ldV, int64_t ignore_index, int write_grad) {
+  __shared__ float sm[8], ss[8];
+  const int row = blockIdx.x;
+  T* x = logits + (int64_t)row * ldV;
+  const int tid = threadIdx.x;
+  float m = -INFINITY, s = 0.f;
+  const int Vv = V & ~7;
+  for (int c = tid * 8; c < Vv; c += 256 * 8) {
+    float v[8];
+    load8<T>(x + c, v);
+    float lm = v[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) lm = fmaxf(lm, v[e]);
+    float nm = fmaxf(m, lm);
+    float acc = s * __expf(m - nm);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += __expf(v[e] - nm);
+    m = nm;
+    s = acc;
+  }
+  for (int c = Vv + tid; c < V; c += 256) {
+    float v = (float)x[c];
+    float nm = fmaxf(m, v);
+    s = s * __expf(m - nm) + __expf(v - nm);
+    m = nm;
+  }
+  // block combine of (m, s)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int lane = tid & 63, w = tid >> 6;
+  if (lane == 0) { sm[w] = m; ss[w] = s; }
+  __syncthreads();
+  float M = sm[0];
+  for (int i = 1; i < 4; ++i) M = fmaxf(M, sm[i]);
+  float Ssum = 0.f;
+  for (int i = 0; i < 4; ++i) Ssum += ss[i] * __expf(sm[i] - M);
+  const float lse = M + __logf(Ssum);
+  const int64_t lab = labels[row];
+  const bool valid = lab != ignore_index && lab >= 0 && lab < V;
+  if (tid == 0) {
+    float xl = valid ? (float)x[lab] : 0.f;
+    loss[row] = valid ? (lse - xl) : 0.f;
+    if (lse_out) lse_out[row] = lse;
+  }
+  if (!write_grad) return;
+  __syncthreads();  // everyone has read x[lab] before it is overwritten
+  for (int c = tid * 8; c < ldV; c += 256 * 8) {
+    float v[8];
+    if (c + 8 <= Vv) {
+      load8<T>(x + c, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float p = valid ? __expf(v[e] - lse) : 0.f;
+        if (valid && c + e == lab) p -= 1.f;
+        v[e] = p;
+      }
+      store8<T>(x + c, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        int cc = c + e;
+        if (cc >= ldV) break;
+        float p = 0.f;
+        if (cc < V && valid) {
+          p = __expf((float)x[cc] - lse);
+          if (cc == lab) p -= 1.f;
+        }
+        x[cc] = (T)p;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// logits [M, ldV] (modified in place into dlogits when write_grad) -> (loss[M], lse[M])
+std::vector<at::Tensor> mift_xent_fwd_bwd(at::Tensor& logits, const at::Tensor& labels, int64_t V,
+                                          int64_t ignore_index, bool write_grad) {
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "xent: 2-D row-major logits");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0), "xent: labels");
+  const int M = logits.size(0), ldV = logits.stride(0);
+  TORCH_CHECK(ldV % 8 == 0 && V <= logits.size(1), "xent: ldV % 8");
+  auto loss = at::empty({M}, logits.options().dtype(at::kFloat));
+  auto lse = at::empty({M}, logits.options().dtype(at::kFloat));
+  if (M == 0) return {loss, lse};
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  auto lab = labels.contiguous();
+  if (logits.scalar_type() == at::kBFloat16)
+    xent_kernel<bf16><<<M, 256, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                         lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0);
+  else if (logits.scalar_type() == at::kHalf)
+    xent_kernel<fp16><<<M, 256, 0, st>>>((fp16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                         lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0);
+  else
+    xent_kernel<float><<<M, 256, 0, st>>>((float*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                          lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0);
+  return {loss, lse};
+}

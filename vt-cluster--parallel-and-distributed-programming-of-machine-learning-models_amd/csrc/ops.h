@@ -17,7 +17,36 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                                      int64_t act, const c10::optional<at::Tensor>& aux,
                                      const c10::optional<at::Tensor>& residual, double dropout_p, int64_t seed,
                                      bool want_preact, double alpha, const c10::optional<at::Tensor>& out,
-                                     int64_t tile);
+                                     int64_t tile, const c10::optional<at::Tensor>& alpha_t,
+                                     const c10::optional<at::Tensor>& pre_add);
+
+// ---- elementwise / embedding / LoRA pack (kernels/elementwise.hip)
+at::Tensor mift_mask_scale(const at::Tensor& x, double p, int64_t seed, const c10::optional<at::Tensor>& out,
+                           bool accumulate);
+at::Tensor mift_act_bwd(const at::Tensor& g, const at::Tensor& z, int64_t act, double p, int64_t seed);
+at::Tensor mift_embed_fwd(const at::Tensor& ids, const c10::optional<at::Tensor>& pos, const at::Tensor& wte,
+                          const c10::optional<at::Tensor>& wpe, int64_t pos_offset, double p, int64_t seed,
+                          at::ScalarType out_dtype);
+std::vector<at::Tensor> mift_pack_lora(const at::Tensor& A, const at::Tensor& B, double a_scale, at::ScalarType dt);
+
+// ---- K7 cross-entropy (kernels/xent.hip)
+std::vector<at::Tensor> mift_xent_fwd_bwd(at::Tensor& logits, const at::Tensor& labels, int64_t V,
+                                          int64_t ignore_index, bool write_grad);
+
+// ---- K9 fused optimizer (kernels/adamw.hip)
+void mift_grad_stats(const at::Tensor& g, at::Tensor& stats);
+void mift_opt_finalize(const at::Tensor& stats, at::Tensor& state, double max_norm, bool dynamic_scale,
+                       double growth_factor, double backoff_factor, int64_t growth_interval);
+void mift_adamw(at::Tensor& p, at::Tensor& g, at::Tensor& m, at::Tensor& v, const at::Tensor& lr_t,
+                const at::Tensor& state, double beta1, double beta2, double eps, double wd);
 
 #define MIFT_BIND_MORE(m) \
-  m.def("gemm_nt", &mift_gemm_nt, "C = epi(A @ B^T [+ A2 @ B2^T]) MFMA bf16/fp16");
+  m.def("gemm_nt", &mift_gemm_nt, "C = epi(A @ B^T [+ A2 @ B2^T]) MFMA bf16/fp16"); \
+  m.def("grad_stats", &mift_grad_stats, "sum(g^2), nonfinite count -> stats[2]"); \
+  m.def("opt_finalize", &mift_opt_finalize, "clip coef / found_inf / step / loss-scale update"); \
+  m.def("adamw", &mift_adamw, "fused AdamW over a flat fp32 arena (zeroes grads)"); \
+  m.def("mask_scale", &mift_mask_scale, "counter-hash dropout (fwd == bwd), optional accumulate"); \
+  m.def("act_bwd", &mift_act_bwd, "dz = dropmask(g) * act'(z)"); \
+  m.def("embed_fwd", &mift_embed_fwd, "token + position gather (+dropout)"); \
+  m.def("pack_lora", &mift_pack_lora, "fp32 LoRA A,B -> padded 16-bit A32[32,K], B32[N,32]"); \
+  m.def("xent_fwd_bwd", &mift_xent_fwd_bwd, "row cross-entropy; dlogits written in place");

@@ -1,0 +1,60 @@
+"""K3 causal self-attention entry point.
+
+``causal_attention(qkv, B, S, H, hd, ...)`` takes the fused projection output
+[B, S, 3*H*hd] (q | k | v, heads interleaved as HF GPT-2 / OPT split them)
+and returns [B, S, H*hd].  GPU tensors run the gfx950 flash-attention
+kernels (csrc/kernels/attention.hip) when available for the head dim;
+otherwise (CPU) the reference path.
+"""
+import torch
+import torch.nn.functional as Fnn
+
+from . import reference as ref
+from .dispatch import use_kernels, C
+
+
+def _split(qkv, B, S, H, hd):
+    x = qkv.view(B, S, 3, H, hd)
+    return x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+
+
+class _FlashAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, B, S, H, hd, scale, p, seed, kv_len):
+        qkv = qkv.contiguous()
+        o, lse = C().attn_fwd(qkv, B, S, H, hd, float(scale), float(p), int(seed), kv_len)
+        ctx.save_for_backward(qkv, o, lse, kv_len if kv_len is not None else torch.empty(0))
+        ctx.meta = (B, S, H, hd, scale, p, seed, kv_len is not None)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, kv_len = ctx.saved_tensors
+        B, S, H, hd, scale, p, seed, has_len = ctx.meta
+        dqkv = C().attn_bwd(do.contiguous(), qkv, o, lse, B, S, H, hd, float(scale), float(p), int(seed),
+                            kv_len if has_len else None)
+        return dqkv, None, None, None, None, None, None, None, None
+
+
+def flash_supported(hd):
+    try:
+        return hasattr(C(), "attn_fwd") and hd in (32, 64, 80, 128)
+    except Exception:
+        return False
+
+
+def causal_attention(qkv, B, S, H, hd, scale=None, dropout_p=0.0, seed=0, kv_len=None):
+    scale = scale if scale is not None else hd ** -0.5
+    if use_kernels(qkv) and flash_supported(hd):
+        o = _FlashAttn.apply(qkv.reshape(B * S, 3 * H * hd), B, S, H, hd, scale, dropout_p, seed, kv_len)
+        return o.view(B, S, H * hd)
+    q, k, v = _split(qkv, B, S, H, hd)
+    if qkv.is_cuda:
+        # GPU without the flash kernel for this head dim: torch SDPA (its own RNG for dropout)
+        o = Fnn.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True, scale=scale)
+    else:
+        valid = None
+        if kv_len is not None:
+            valid = torch.arange(S, device=qkv.device)[None, :] < kv_len[:, None]
+        o = ref.attention(q, k, v, causal=True, key_padding=valid, scale=scale, dropout_p=dropout_p, seed=seed)
+    return o.transpose(1, 2).reshape(B, S, H * hd)

@@ -1,0 +1,252 @@
+"""Data-parallel LoRA trainer (replaces HF Trainer + torch DDP, reference C16/C21/C35).
+
+Semantics kept from the reference (HF Trainer defaults):
+  * per-rank micro-batch ``batch`` x ``accum`` micro-steps per optimizer step;
+  * loss normalised by the number of label tokens in the whole optimizer
+    step across all DP ranks (Trainer's ``num_items_in_batch`` path), so
+    ``batch=1, accum=32`` and ``batch=32, accum=1`` give the same update;
+  * AdamW(β=(0.9,0.999), eps 1e-8, wd 0), global-norm clip 1.0, linear LR
+    decay to 0 with no warmup;
+  * ``no_sync`` on accumulation micro-steps, one gradient all-reduce per
+    optimizer step;
+  * step / phase log lines in the reference formats (mift.obs.timing);
+  * checkpoint-N dirs every ``save_steps`` (adapter, optimizer, rng,
+    trainer_state.json, data position) + ``resume='auto'``.
+
+MI355X-specific: bf16 (default) / fp16 with device-side dynamic loss scaling
+/ fp32; the optimizer step, clip and loss scale never sync the host; the
+host only syncs at logging steps.
+"""
+import json
+import math
+import os
+import shutil
+import time
+from dataclasses import dataclass, asdict, field
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..lora import LoraArena, adapter_state_dict, save_adapter
+from ..obs.timing import HOST, hf_log_line, lab_step_line, p1_step_line
+from ..parallel.ddp import GradReducer
+from ..utils.faults import maybe_inject
+from .optim import FusedAdamW, linear_schedule
+
+
+@dataclass
+class TrainConfig:
+    epochs: float = 1.0
+    batch: int = 1
+    accum: int = 32
+    lr: float = 5e-5
+    warmup_steps: int = 0
+    weight_decay: float = 0.0
+    max_grad_norm: float = 1.0
+    precision: str = "bf16"           # bf16 | fp16 | fp32
+    logging_steps: int = 50
+    save_steps: int = 500
+    save_total_limit: int = 1
+    max_steps: int = -1
+    seed: int = 0
+    output_dir: Optional[str] = None
+    resume: Optional[str] = None       # None | 'auto' | path
+    step_log: str = "p1"               # p1 | lab | none
+    bucket_mb: float = 25.0
+    recompute: bool = False
+    shuffle: bool = False
+
+
+class Trainer:
+    def __init__(self, model, batcher, cfg: TrainConfig, ctx=None, callbacks=()):
+        self.model, self.batcher, self.cfg, self.ctx = model, batcher, cfg, ctx
+        self.rank = ctx.rank if ctx else 0
+        self.device = ctx.device if ctx else torch.device("cpu")
+        self.dp_group = ctx.dp_group if ctx else None
+        self.dp = ctx.dp if ctx else 1
+        self.arena = LoraArena(model, device=self.device)
+        self.reducer = GradReducer(self.arena, group=self.dp_group, bucket_mb=cfg.bucket_mb, world=self.dp)
+        self.opt = FusedAdamW(self.arena.param, self.arena.grad, lr=cfg.lr, weight_decay=cfg.weight_decay,
+                              max_grad_norm=cfg.max_grad_norm,
+                              loss_scale="dynamic" if cfg.precision == "fp16" else "none")
+        spe = batcher.steps_per_epoch()
+        self.steps_per_epoch = spe
+        total = int(math.ceil(spe * cfg.epochs))
+        if cfg.max_steps > 0:
+            total = min(total, cfg.max_steps)
+        self.total_steps = total
+        self.sched = linear_schedule(cfg.lr, total, cfg.warmup_steps)
+        self.global_step = 0
+        self.callbacks = list(callbacks)
+        self.history = []
+        model.recompute = cfg.recompute
+        self._ctrl = ctx.ctrl_group if ctx else None
+
+    # ------------------------------------------------------------------
+    def _global_tokens(self, mbs):
+        n = sum(int((mb["labels"][:, 1:] != -100).sum()) for mb in mbs)
+        if self.dp > 1 and dist.is_initialized():
+            t = torch.tensor([n], dtype=torch.float64)
+            dist.all_reduce(t, group=self._dp_ctrl_group())
+            n = int(t.item())
+        return max(n, 1)
+
+    def _dp_ctrl_group(self):
+        if not hasattr(self, "_dpc"):
+            self._dpc = None
+            if self.ctx is not None and self.ctx.dp > 1:
+                if self.ctx.pp == 1:
+                    self._dpc = self.ctx.ctrl_group
+                else:
+                    # gloo mirror of the DP group (created collectively on all ranks)
+                    groups = {}
+                    for s in range(self.ctx.pp):
+                        ranks = list(range(s, self.ctx.world, self.ctx.pp))
+                        groups[s] = dist.new_group(ranks, backend="gloo")
+                    self._dpc = groups[self.ctx.pp_rank]
+        return self._dpc
+
+    def _to_dev(self, mb):
+        return {k: v.to(self.device, non_blocking=True) for k, v in mb.items()}
+
+    def train_step(self, mbs):
+        """One optimizer step over a list of micro-batches. Returns loss_sum tensor."""
+        model, cfg = self.model, self.cfg
+        ntok = self._global_tokens(mbs)
+        lr = self.sched(self.global_step)
+        self.opt.set_lr(lr)
+        gscale = self.opt.loss_scale_t / ntok
+        loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
+        autocast = (self.device.type == "cpu" and cfg.precision == "bf16")
+        for i, mb in enumerate(mbs):
+            mb = self._to_dev(mb)
+            model.next_micro_step()
+            last = i == len(mbs) - 1
+            ctxm = self.reducer.no_sync() if not last else _null()
+            with ctxm:
+                with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+                    out = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"],
+                                labels=mb["labels"], reduction="sum", return_logits=False)
+                loss_sum = out["loss"].float()
+                (loss_sum * gscale).backward()
+            loss_acc += loss_sum.detach()
+            maybe_inject(self.rank, self.global_step + 1, "micro")
+        self.arena.rebind_grads()
+        self.reducer.finish()
+        self.opt.step()
+        self.global_step += 1
+        return loss_acc, ntok
+
+    # ------------------------------------------------------------------
+    def train(self):
+        cfg = self.cfg
+        start_step = 0
+        if cfg.resume:
+            start_step = self.resume(cfg.resume)
+        self.model.train()
+        t_last = time.perf_counter()
+        sync_dev = self.device.type == "cuda"
+        epoch = start_step // max(1, self.steps_per_epoch)
+        done = start_step >= self.total_steps
+        log_loss, log_tok = 0.0, 0
+        while not done:
+            skip = start_step - epoch * self.steps_per_epoch
+            for mbs in self.batcher.epoch(epoch, start_step=max(0, skip)):
+                loss_sum, ntok = self.train_step(mbs)
+                maybe_inject(self.rank, self.global_step, "step")
+                if cfg.step_log != "none" or (cfg.logging_steps and self.global_step % cfg.logging_steps == 0):
+                    if sync_dev:
+                        torch.cuda.synchronize()
+                    now = time.perf_counter()
+                    dt = now - t_last
+                    t_last = now
+                    if cfg.step_log == "p1":
+                        print(p1_step_line(self.rank, self.global_step, dt), flush=True)
+                    elif cfg.step_log == "lab":
+                        samples = cfg.batch * len(mbs) * self.dp
+                        sps = samples / max(dt, 1e-9)
+                        seq = mbs[0]["input_ids"].shape[1]
+                        print(lab_step_line(self.rank, self.global_step, dt * 1000, sps, sps * seq), flush=True)
+                log_loss += float(loss_sum) if (cfg.logging_steps and self.global_step % cfg.logging_steps == 0) else 0.0
+                if cfg.logging_steps and self.global_step % cfg.logging_steps == 0:
+                    st = self.opt.stats()
+                    rec = {"loss": float(loss_sum) / max(1, ntok) * (self.dp if False else 1),
+                           "grad_norm": st["grad_norm"], "learning_rate": self.sched(self.global_step),
+                           "epoch": round(self.global_step / max(1, self.steps_per_epoch), 4)}
+                    self.history.append(dict(rec, step=self.global_step))
+                    if self.rank == 0:
+                        print(hf_log_line(rec), flush=True)
+                    for cb in self.callbacks:
+                        cb(self, rec)
+                if cfg.output_dir and cfg.save_steps and self.global_step % cfg.save_steps == 0:
+                    self.save_checkpoint()
+                if self.global_step >= self.total_steps:
+                    done = True
+                    break
+            epoch += 1
+            start_step = epoch * self.steps_per_epoch
+            if epoch * self.steps_per_epoch >= self.total_steps:
+                done = True
+        if sync_dev:
+            torch.cuda.synchronize()
+        return self.history
+
+    # ------------------------------------------------------------------
+    def save_checkpoint(self):
+        """``checkpoint-<step>/``: adapter + optimizer + rng + trainer_state (+rotation)."""
+        out = os.path.join(self.cfg.output_dir, f"checkpoint-{self.global_step}")
+        if self.rank == 0:
+            os.makedirs(out, exist_ok=True)
+            save_adapter(out, adapter_state_dict(self.model), self.model.lora_config)
+            torch.save(self.opt.state_dict(), os.path.join(out, "optimizer.pt"))
+            with open(os.path.join(out, "trainer_state.json"), "w") as f:
+                json.dump({"global_step": self.global_step, "max_steps": self.total_steps,
+                           "steps_per_epoch": self.steps_per_epoch, "log_history": self.history,
+                           "micro_step": self.model.micro_step, "seed": self.model.seed}, f, indent=2)
+        if dist.is_initialized():
+            dist.barrier(group=self.ctx.ctrl_group if self.ctx else None)
+        torch.save({"cpu": torch.get_rng_state()}, os.path.join(out, f"rng_state_{self.rank}.pth"))
+        if self.rank == 0 and self.cfg.save_total_limit:
+            cks = sorted([d for d in os.listdir(self.cfg.output_dir) if d.startswith("checkpoint-")],
+                         key=lambda d: int(d.split("-")[1]))
+            for d in cks[:-self.cfg.save_total_limit]:
+                shutil.rmtree(os.path.join(self.cfg.output_dir, d), ignore_errors=True)
+        return out
+
+    def resume(self, spec):
+        path = spec
+        if spec == "auto":
+            if not self.cfg.output_dir or not os.path.isdir(self.cfg.output_dir):
+                return 0
+            cks = [d for d in os.listdir(self.cfg.output_dir) if d.startswith("checkpoint-")]
+            if not cks:
+                return 0
+            path = os.path.join(self.cfg.output_dir, max(cks, key=lambda d: int(d.split("-")[1])))
+        from ..lora import load_adapter
+        load_adapter(self.model, path)
+        self.opt.load_state_dict(torch.load(os.path.join(path, "optimizer.pt"), weights_only=True))
+        with open(os.path.join(path, "trainer_state.json")) as f:
+            st = json.load(f)
+        self.global_step = st["global_step"]
+        self.history = st.get("log_history", [])
+        self.model.micro_step = st.get("micro_step", 0)
+        rp = os.path.join(path, f"rng_state_{self.rank}.pth")
+        if os.path.exists(rp):
+            torch.set_rng_state(torch.load(rp, weights_only=True)["cpu"])
+        if self.rank == 0:
+            print(f"[resume] from {path} at step {self.global_step}", flush=True)
+        return self.global_step
+
+
+@torch.no_grad()
+def _noop():
+    pass
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
