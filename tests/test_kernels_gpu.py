@@ -140,3 +140,47 @@ def test_mask_scale_and_embed():
     h = C.embed_fwd(ids, None, wte, wpe, 0, 0.0, 0, torch.bfloat16)
     e = (wte[ids].float() + wpe[torch.arange(32, device="cuda")][None].float()).view(-1, 64)
     torch.testing.assert_close(h.float(), e, atol=2e-2, rtol=1e-2)
+
+
+def _attn_ref(qkv, B, S, H, hd, scale, p, seed, kv_len=None):
+    q, k, v = qkv.float().view(B, S, 3, H, hd).unbind(2)
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    valid = None
+    if kv_len is not None:
+        valid = torch.arange(S, device=qkv.device)[None, :] < kv_len[:, None]
+    o = ref.attention(q, k, v, causal=True, key_padding=valid, scale=scale, dropout_p=p, seed=seed)
+    return o.transpose(1, 2).reshape(B * S, H * hd)
+
+
+@pytest.mark.parametrize("hd", [64, 80, 128])
+@pytest.mark.parametrize("S", [256, 200])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention_fwd_bwd(hd, S, p):
+    C = _C()
+    torch.manual_seed(6)
+    B, H = 2, 3
+    scale = hd ** -0.5
+    qkv = (torch.randn(B * S, 3 * H * hd, device="cuda")).to(torch.bfloat16)
+    o, lse = C.attn_fwd(qkv, B, S, H, hd, scale, p, 321, None)
+    x = qkv.float().requires_grad_(True)
+    oref = _attn_ref(x, B, S, H, hd, scale, p, 321)
+    torch.testing.assert_close(o.float(), oref, atol=3e-2, rtol=3e-2)
+    do = torch.randn_like(o)
+    oref.backward(do.float())
+    dqkv = C.attn_bwd(do, qkv, o, lse, B, S, H, hd, scale, p, 321, None)
+    g = x.grad.view(B * S, 3, H * hd)
+    dq = dqkv.float().view(B * S, 3, H * hd)
+    for i, name in enumerate("qkv"):
+        err = (dq[:, i] - g[:, i]).norm() / (g[:, i].norm() + 1e-6)
+        assert err < 3e-2, f"d{name} rel err {err:.3e}"
+
+
+def test_flash_attention_kv_len():
+    C = _C()
+    torch.manual_seed(7)
+    B, S, H, hd = 2, 128, 2, 64
+    qkv = torch.randn(B * S, 3 * H * hd, device="cuda").to(torch.bfloat16)
+    kvl = torch.tensor([100, 37], device="cuda", dtype=torch.int32)
+    o, lse = C.attn_fwd(qkv, B, S, H, hd, hd ** -0.5, 0.0, 0, kvl)
+    oref = _attn_ref(qkv, B, S, H, hd, hd ** -0.5, 0.0, 0, kvl)
+    torch.testing.assert_close(o.float(), oref, atol=3e-2, rtol=3e-2)

@@ -28,15 +28,54 @@ typedef _Float16 fp16x8 __attribute__((ext_vector_type(8)));
 template <typename T> MIFT_HD float to_f32(T x) { return (float)x; }
 template <typename T> MIFT_HD T from_f32(float x) { return (T)x; }
 
-// splitmix64 finaliser of (seed + idx * golden) -> top 32 bits.
-MIFT_HD uint32_t mift_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return (uint32_t)((z ^ (z >> 31)) >> 32);
+// Counter-based dropout RNG (32-bit ops only: 64-bit multiplies are
+// emulated on CDNA and made the old splitmix64 mask VALU-bound).
+// One 32-bit hash per element PAIR (idx >> 1); element idx uses the low
+// (even idx) or high (odd idx) 16 bits; keep iff bits >= thr16 where
+// thr16 = round(p * 65536).  Unbiased rescale: inv_keep = 65536/(65536-thr16).
+MIFT_HD uint32_t mix32(uint32_t x) {  // "lowbias32" finaliser
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+MIFT_HD uint32_t mift_hash_pair(uint64_t seed, uint64_t pair) {
+  const uint32_t lo = (uint32_t)pair, hi = (uint32_t)(pair >> 32);
+  return mix32((lo * 0x9E3779B9U) ^ mix32(hi ^ (uint32_t)(seed >> 32)) ^ (uint32_t)seed);
+}
+MIFT_HD uint32_t mift_bits16(uint64_t seed, uint64_t idx) {
+  return (mift_hash_pair(seed, idx >> 1) >> ((idx & 1) << 4)) & 0xFFFFu;
+}
+MIFT_HD bool mift_keep(uint64_t seed, uint64_t idx, uint32_t thr) { return mift_bits16(seed, idx) >= thr; }
+// 8 consecutive elements: 4 hashes when idx0 is even (the common case).
+MIFT_HD void mift_keep8(uint64_t seed, uint64_t idx0, uint32_t thr, bool* k) {
+  if ((idx0 & 1) == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const uint32_t h = mift_hash_pair(seed, (idx0 + e) >> 1);
+      k[e] = (h & 0xFFFFu) >= thr;
+      k[e + 1] = (h >> 16) >= thr;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) k[e] = mift_keep(seed, idx0 + e, thr);
+  }
 }
 
-MIFT_HD bool mift_keep(uint64_t seed, uint64_t idx, uint32_t thr) { return mift_hash(seed, idx) >= thr; }
+#ifndef __HIP_DEVICE_COMPILE__
+#include <algorithm>
+#endif
+static inline uint32_t mift_thr16(double p) {
+  if (p <= 0.0) return 0u;
+  double t = p * 65536.0 + 0.5;
+  return (uint32_t)(t > 65536.0 ? 65536.0 : t);
+}
+static inline float mift_inv_keep(double p) {
+  const uint32_t t = mift_thr16(p);
+  return t >= 65536u ? 0.f : (float)(65536.0 / (65536.0 - (double)t));
+}
 
 // GPT-2 "gelu_new" (tanh approximation) and its derivative.
 MIFT_HD float gelu_tanh(float x) {

@@ -23,9 +23,11 @@ __global__ __launch_bounds__(256) void mask_scale_kernel(const T* __restrict__ x
       float v[8], o[8];
       load8<T>(x + i, v);
       if (accumulate) load8<T>(y + i, o);
+      bool kp[8];
+      mift_keep8(seed, (uint64_t)i, thr, kp);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float r = mift_keep(seed, (uint64_t)(i + e), thr) ? v[e] * inv_keep : 0.f;
+        float r = kp[e] ? v[e] * inv_keep : 0.f;
         o[e] = accumulate ? o[e] + r : r;
       }
       store8<T>(y + i, o);
@@ -57,9 +59,11 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ g, c
       float gv[8], zv[8];
       load8<T>(g + i, gv);
       load8<T>(z + i, zv);
+      bool kp[8] = {true, true, true, true, true, true, true, true};
+      if (thr != 0) mift_keep8(seed, (uint64_t)i, thr, kp);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float m = (thr == 0 || mift_keep(seed, (uint64_t)(i + e), thr)) ? inv_keep : 0.f;
+        float m = kp[e] ? inv_keep : 0.f;
         gv[e] = gv[e] * m * act_grad(act, zv[e]);
       }
       store8<T>(out + i, gv);
@@ -85,10 +89,12 @@ __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ 
     load8<W>(wte + tok * D + c, a);
     if (wpe != nullptr) load8<W>(wpe + p * D + c, b);
     else for (int e = 0; e < 8; ++e) b[e] = 0.f;
+    bool kp[8] = {true, true, true, true, true, true, true, true};
+    if (thr != 0) mift_keep8(seed, (uint64_t)row * D + c, thr, kp);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float v = a[e] + b[e];
-      if (thr != 0) v = mift_keep(seed, (uint64_t)row * D + c + e, thr) ? v * inv_keep : 0.f;
+      if (thr != 0) v = kp[e] ? v * inv_keep : 0.f;
       a[e] = v;
     }
     store8<T>(h + (int64_t)row * D + c, a);
@@ -115,7 +121,7 @@ int ew_grid(int64_t n) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, 4096));
 }
 
-uint32_t thr_of(double p) { return p > 0 ? (uint32_t)std::min(4294967295.0, p * 4294967296.0) : 0u; }
+uint32_t thr_of(double p) { return mift_thr16(p); }
 
 }  // namespace
 
@@ -134,7 +140,7 @@ at::Tensor mift_mask_scale(const at::Tensor& x, double p, int64_t seed, const c1
   TORCH_CHECK(y.is_contiguous() && y.numel() == x.numel() && y.scalar_type() == x.scalar_type(), "mask_scale: out");
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const int64_t n = x.numel();
-  float inv = p < 1.0 ? (float)(1.0 / (1.0 - p)) : 0.f;
+  float inv = p > 0 ? mift_inv_keep(p) : 1.f;
   DISPATCH_16(x.scalar_type(), mask_scale_kernel<T><<<ew_grid(n), 256, 0, st>>>((const T*)x.data_ptr(), (T*)y.data_ptr(), n,
                                                                                  (uint64_t)seed, thr_of(p), inv,
                                                                                  accumulate ? 1 : 0));
@@ -146,7 +152,7 @@ at::Tensor mift_act_bwd(const at::Tensor& g, const at::Tensor& z, int64_t act, d
   auto out = at::empty_like(g);
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const int64_t n = g.numel();
-  float inv = p > 0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+  float inv = p > 0 ? mift_inv_keep(p) : 1.f;
   DISPATCH_16(g.scalar_type(), act_bwd_kernel<T><<<ew_grid(n), 256, 0, st>>>((const T*)g.data_ptr(), (const T*)z.data_ptr(),
                                                                               (T*)out.data_ptr(), n, (int)act,
                                                                               (uint64_t)seed, thr_of(p), inv));
@@ -164,7 +170,7 @@ at::Tensor mift_embed_fwd(const at::Tensor& ids, const c10::optional<at::Tensor>
   auto h = at::empty({rows, D}, wte.options().dtype(out_dtype));
   if (rows == 0) return h;
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-  float inv = p > 0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+  float inv = p > 0 ? mift_inv_keep(p) : 1.f;
   TORCH_CHECK(wte.scalar_type() == out_dtype, "embed: table dtype must equal out dtype");
   DISPATCH_16(out_dtype, embed_kernel<T, T><<<rows, 256, 0, st>>>(
                              ids.data_ptr<int64_t>(), pos ? pos->data_ptr<int64_t>() : nullptr, (const T*)wte.data_ptr(),

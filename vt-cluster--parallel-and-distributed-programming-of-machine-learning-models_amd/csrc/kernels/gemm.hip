@@ -256,11 +256,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
       for (int e = 0; e < 8; ++e) z[e] = apply_act(ep.act, z[e], ax[e]);
     }
     if (ep.thr != 0) {
+      bool kp[8];
+      mift_keep8(ep.seed, (uint64_t)gr * N + gc, ep.thr, kp);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        uint64_t idx = (uint64_t)gr * N + gc + e;
-        z[e] = mift_keep(ep.seed, idx, ep.thr) ? z[e] * ep.inv_keep : 0.f;
-      }
+      for (int e = 0; e < 8; ++e) z[e] = kp[e] ? z[e] * ep.inv_keep : 0.f;
     }
     if (ep.residual != nullptr) {
       float rv[8];
@@ -351,8 +350,8 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     ep.residual = residual->data_ptr();
   }
   ep.seed = (uint64_t)seed;
-  ep.thr = dropout_p > 0 ? (uint32_t)std::min(4294967295.0, dropout_p * 4294967296.0) : 0u;
-  ep.inv_keep = dropout_p > 0 ? (float)(1.0 / (1.0 - dropout_p)) : 1.f;
+  ep.thr = mift_thr16(dropout_p);
+  ep.inv_keep = dropout_p > 0 ? mift_inv_keep(dropout_p) : 1.f;
   ep.alpha = (float)alpha;
   ep.alpha_ptr = nullptr;
   if (alpha_t) {

@@ -266,8 +266,8 @@ std::vector<at::Tensor> mift_layer_norm_bwd(const at::Tensor& dy, const at::Tens
     dw = at::zeros({D}, x.options().dtype(at::kFloat));
     db = at::zeros({D}, x.options().dtype(at::kFloat));
   }
-  uint32_t thr = (uint32_t)std::min(4294967295.0, p * 4294967296.0);
-  float inv_keep = p < 1.0 ? (float)(1.0 / (1.0 - p)) : 0.f;
+  uint32_t thr = mift_thr16(p);
+  float inv_keep = p > 0 ? mift_inv_keep(p) : 1.f;
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   DISPATCH_TW(x.scalar_type(), w.scalar_type(),
               launch_bwd<T, W>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, (uint64_t)seed, thr,

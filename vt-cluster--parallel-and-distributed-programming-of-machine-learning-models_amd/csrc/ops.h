@@ -40,7 +40,16 @@ void mift_opt_finalize(const at::Tensor& stats, at::Tensor& state, double max_no
 void mift_adamw(at::Tensor& p, at::Tensor& g, at::Tensor& m, at::Tensor& v, const at::Tensor& lr_t,
                 const at::Tensor& state, double beta1, double beta2, double eps, double wd);
 
+// ---- K3 flash attention (kernels/attention.hip)
+std::vector<at::Tensor> mift_attn_fwd(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, int64_t HD, double scale,
+                                      double p, int64_t seed, const c10::optional<at::Tensor>& kv_len);
+at::Tensor mift_attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
+                         int64_t B, int64_t S, int64_t H, int64_t HD, double scale, double p, int64_t seed,
+                         const c10::optional<at::Tensor>& kv_len);
+
 #define MIFT_BIND_MORE(m) \
+  m.def("attn_fwd", &mift_attn_fwd, "causal flash attention fwd on fused qkv -> (o, lse)"); \
+  m.def("attn_bwd", &mift_attn_bwd, "causal flash attention bwd -> dqkv"); \
   m.def("gemm_nt", &mift_gemm_nt, "C = epi(A @ B^T [+ A2 @ B2^T]) MFMA bf16/fp16"); \
   m.def("grad_stats", &mift_grad_stats, "sum(g^2), nonfinite count -> stats[2]"); \
   m.def("opt_finalize", &mift_opt_finalize, "clip coef / found_inf / step / loss-scale update"); \

@@ -12,31 +12,40 @@ import math
 import torch
 import torch.nn.functional as F
 
-_M64 = (1 << 64)
+_M32 = 0xFFFFFFFF
 
 
-def _s64(x: int) -> int:
-    """Reinterpret an unsigned 64-bit constant as signed int64."""
-    return x - _M64 if x >= (1 << 63) else x
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    """lowbias32 on uint32 values held in int64 tensors (matches csrc/common.h)."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    x = x ^ (x >> 16)
+    return x
 
 
-_G = _s64(0x9E3779B97F4A7C15)
-_C1 = _s64(0xBF58476D1CE4E5B9)
-_C2 = _s64(0x94D049BB133111EB)
+def mift_hash_pair(seed: int, pair: torch.Tensor) -> torch.Tensor:
+    seed &= (1 << 64) - 1
+    lo = pair & _M32
+    hi = (pair >> 32) & _M32
+    s_lo, s_hi = seed & _M32, (seed >> 32) & _M32
+    return _mix32(((lo * 0x9E3779B9) & _M32) ^ _mix32(hi ^ s_hi) ^ s_lo)
 
 
-def _lsr(z: torch.Tensor, k: int) -> torch.Tensor:
-    # logical right shift on int64 (torch >> is arithmetic)
-    return (z >> k) & ((1 << (64 - k)) - 1)
+def mift_bits16(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    idx = idx.to(torch.int64)
+    h = mift_hash_pair(seed, idx >> 1)
+    return (h >> ((idx & 1) * 16)) & 0xFFFF
 
 
-def mift_hash(seed: int, idx: torch.Tensor) -> torch.Tensor:
-    """splitmix64 finaliser of (seed + idx*golden); returns top 32 bits as int64."""
-    z = torch.as_tensor(_s64(seed % _M64), dtype=torch.int64) + idx.to(torch.int64) * _G
-    z = (z ^ _lsr(z, 30)) * _C1
-    z = (z ^ _lsr(z, 27)) * _C2
-    z = z ^ _lsr(z, 31)
-    return _lsr(z, 32)
+def thr16(p: float) -> int:
+    return 0 if p <= 0 else min(int(p * 65536.0 + 0.5), 65536)
+
+
+def inv_keep(p: float) -> float:
+    t = thr16(p)
+    return 1.0 if t == 0 else (0.0 if t >= 65536 else 65536.0 / (65536.0 - t))
 
 
 def keep_mask(seed: int, shape, p: float, device=None) -> torch.Tensor:
@@ -45,15 +54,14 @@ def keep_mask(seed: int, shape, p: float, device=None) -> torch.Tensor:
     for s in shape:
         n *= int(s)
     idx = torch.arange(n, dtype=torch.int64, device=device)
-    thr = min(int(p * 4294967296.0), 4294967295)
-    return (mift_hash(seed, idx) >= thr).view(*shape)
+    return (mift_bits16(seed, idx) >= thr16(p)).view(*shape)
 
 
 def dropout(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
     if p <= 0.0:
         return x
     m = keep_mask(seed, x.shape, p, x.device)
-    return torch.where(m, x / (1.0 - p), torch.zeros((), dtype=x.dtype, device=x.device))
+    return torch.where(m, x * inv_keep(p), torch.zeros((), dtype=x.dtype, device=x.device))
 
 
 def gelu_new(x: torch.Tensor) -> torch.Tensor:
