@@ -55,3 +55,22 @@ def test_fused_dropout_runs_and_is_deterministic():
     a = fused(input_ids=ids, labels=ids, reduction="sum")["loss"].item()
     b = fused(input_ids=ids, labels=ids, reduction="sum")["loss"].item()
     assert abs(a - b) < 1e-3 * abs(a)  # same micro_step -> same masks (flash path) or close (sdpa)
+
+
+def test_arena_pack_path_matches_dense_path():
+    """Trainer fast path (packed operands + grads written into the arena) == per-module path."""
+    from mift.lora import LoraArena
+    from mift.lora.pack import attach
+    cfg, ref, fused = _models(0.0)
+    fused2 = copy.deepcopy(fused)
+    ids = torch.randint(0, cfg.vocab_size, (4, 64), device="cuda")
+    fused.train()
+    fused2.train()
+    fused(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
+    arena = LoraArena(fused2)
+    attach(fused2, arena, torch.bfloat16)
+    fused2(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
+    for (n1, p1), (n2, p2) in zip(L.lora_parameters(fused), L.lora_parameters(fused2)):
+        g1, g2 = p1.grad.float(), p2.grad.float()
+        rel = (g1 - g2).norm() / (g1.norm() + 1e-6)
+        assert rel < 2e-2, f"{n1}: rel err {rel:.3e}"

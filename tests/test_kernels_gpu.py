@@ -44,7 +44,7 @@ def test_gemm_nt_plain(M, N, K):
     torch.manual_seed(1)
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
-    out = C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None)[0]
+    out = C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
     exp = a.float() @ b.float().t()
     torch.testing.assert_close(out.float(), exp, atol=3e-2, rtol=2e-2)
 
@@ -55,7 +55,7 @@ def test_gemm_nt_identity_asymmetric():
     n = 128
     a = torch.eye(n, device="cuda", dtype=torch.bfloat16)
     bm = (torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
-    out = C.gemm_nt(a, bm, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None)[0]
+    out = C.gemm_nt(a, bm, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
     torch.testing.assert_close(out.float(), bm.float().t())
 
 
@@ -70,7 +70,7 @@ def test_gemm_nt_fused_epilogue(act):
     a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
     b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
     res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-    out, pre = C.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True, 1.0, None, 0, None, None)
+    out, pre = C.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True, 1.0, None, 0, None, None, 0.0, 0)
     exp, exp_pre = ref.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True)
     torch.testing.assert_close(pre.float(), exp_pre.float(), atol=5e-2, rtol=2e-2)
     torch.testing.assert_close(out.float(), exp.float(), atol=8e-2, rtol=3e-2)
@@ -84,7 +84,7 @@ def test_gemm_nt_act_backward(act):
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
     aux = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-    out = C.gemm_nt(a, b, None, None, None, act, aux, None, 0.0, 0, False, 1.0, None, 0, None, None)[0]
+    out = C.gemm_nt(a, b, None, None, None, act, aux, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
     exp, _ = ref.gemm_nt(a, b, None, None, None, act, aux)
     torch.testing.assert_close(out.float(), exp.float(), atol=5e-2, rtol=3e-2)
 
@@ -184,3 +184,35 @@ def test_flash_attention_kv_len():
     o, lse = C.attn_fwd(qkv, B, S, H, hd, hd ** -0.5, 0.0, 0, kvl)
     oref = _attn_ref(qkv, B, S, H, hd, hd ** -0.5, 0.0, 0, kvl)
     torch.testing.assert_close(o.float(), oref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.05])
+def test_lora_proj_and_wgrad(p):
+    C = _C()
+    torch.manual_seed(8)
+    M, K = 1000, 768
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.zeros(32, K, device="cuda", dtype=torch.bfloat16)
+    w[:8] = (torch.randn(8, K, device="cuda") * 0.05).to(torch.bfloat16)
+    out = C.lora_proj(x, w, 2.0, p, 55)
+    xd = ref.dropout(x.float(), p, 55)
+    torch.testing.assert_close(out.float(), 2.0 * xd @ w.float().t(), atol=3e-2, rtol=3e-2)
+    y = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
+    acc = torch.zeros(K, 32, device="cuda")
+    C.lora_wgrad(x, y, acc, p, 55, 0, 32, 0)
+    exp = xd.t() @ y.float()
+    err = (acc - exp).norm() / exp.norm()
+    assert err < 1e-2, err
+
+
+def test_gemm_ext_masked():
+    C = _C()
+    torch.manual_seed(9)
+    M, N, K = 512, 768, 256
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
+    b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
+    out = C.gemm_nt(a, b, None, a2, b2, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.05, 1234)[0]
+    exp = a.float() @ b.float().t() + ref.dropout(a2.float() @ b2.float().t(), 0.05, 1234)
+    torch.testing.assert_close(out.float(), exp, atol=5e-2, rtol=3e-2)

@@ -62,7 +62,7 @@ def bench_gemm(results):
         fl = 2.0 * M * N * K
         row = {"name": name, "M": M, "N": N, "K": K}
         for tile in (0, 1, 2, 3):
-            t = timeit(lambda: C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, tile))
+            t = timeit(lambda: C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, tile, None, None, 0.0, 0))
             row[f"mift_t{tile}_ms"] = round(t, 4)
             row[f"mift_t{tile}_tflops"] = round(fl / t / 1e9, 1)
         t = timeit(lambda: torch.matmul(a, b.t()))

@@ -78,16 +78,18 @@ static inline float mift_inv_keep(double p) {
 }
 
 // GPT-2 "gelu_new" (tanh approximation) and its derivative.
+// tanh via one v_exp_f32 + one fast divide (saturates correctly at +-inf)
+MIFT_HD float fast_tanh(float u) { return 1.f - __fdividef(2.f, 1.f + __expf(2.f * u)); }
 MIFT_HD float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return 0.5f * x * (1.f + fast_tanh(u));
 }
 MIFT_HD float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float x2 = x * x;
   float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
+  float t = fast_tanh(u);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 MIFT_HD float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }

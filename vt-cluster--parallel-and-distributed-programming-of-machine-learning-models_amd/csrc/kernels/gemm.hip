@@ -60,6 +60,9 @@ struct EpiArgs {
   float alpha;       // acc scale
   const float* alpha_ptr;  // optional device-side extra scale (e.g. upstream grad / loss scale)
   const void* pre_add;     // [M,N] T added to z before the activation
+  uint32_t ext_thr;        // != 0: K-extension product is dropout-masked (LoRA input-dropout backward)
+  uint64_t ext_seed;
+  float ext_inv_keep;
 };
 
 template <typename T>
@@ -185,23 +188,30 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
   }
 
   // ---- LoRA K-extension: one extra K=32 step from global (A2[M,32], B2[N,32]) ----
-  if (A2 != nullptr) {
-    frag_t<T> af[TM], bfv[TN];
+  // ext_thr == 0: accumulated into acc (forward: y += T·B^T).
+  // ext_thr != 0: kept separate and added in phase 1 under the dropout mask
+  //               (dgrad: dX += keep ⊙ (s·dT·A)/(1-p), mask of the LoRA input).
+  frag_t<T> af2[TM], bf2[TN];
+  const bool ext = A2 != nullptr;
+  if (ext) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       int r = min(m0 + wm * WM + i * 16 + fr, M - 1);
-      af[i] = *reinterpret_cast<const frag_t<T>*>(A2 + (size_t)r * 32 + fq * 8);
+      af2[i] = *reinterpret_cast<const frag_t<T>*>(A2 + (size_t)r * 32 + fq * 8);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       int r = min(n0 + wn * WN + j * 16 + fr, N - 1);
-      bfv[j] = *reinterpret_cast<const frag_t<T>*>(B2 + (size_t)r * 32 + fq * 8);
+      bf2[j] = *reinterpret_cast<const frag_t<T>*>(B2 + (size_t)r * 32 + fq * 8);
     }
+    if (ep.ext_thr == 0) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(af[i], bfv[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(af2[i], bf2[j], acc[i][j]);
+    }
   }
+  const bool ext_masked = ext && ep.ext_thr != 0;
 
   // ---- epilogue phase 1: acc (*alpha, +bias) -> T tile in LDS [BM][BN] ----
   T* Cs = reinterpret_cast<T*>(smem);
@@ -216,10 +226,33 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
                        : (float)reinterpret_cast<const T*>(ep.bias)[n0 + col];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      float4_ xt = float4_{0.f, 0.f, 0.f, 0.f};
+      uint32_t hb[4] = {0, 0, 0, 0};
+      if (ext_masked) {
+        xt = mfma16<T>(af2[i], bf2[j], xt);
+        // lanes fr and fr^1 hold columns (2c, 2c+1) = one hash pair per row:
+        // the even lane hashes rows e=0,1, the odd lane rows e=2,3, then swap.
+        const int rbase = m0 + wm * WM + i * 16 + fq * 4;
+        const int odd = fr & 1;
+        const uint64_t p0 = ((uint64_t)(rbase + 2 * odd) * N + n0 + col) >> 1;
+        const uint64_t p1 = ((uint64_t)(rbase + 2 * odd + 1) * N + n0 + col) >> 1;
+        const uint32_t h0 = mift_hash_pair(ep.ext_seed, p0), h1 = mift_hash_pair(ep.ext_seed, p1);
+        const uint32_t o0 = __shfl_xor(h0, 1, 64), o1 = __shfl_xor(h1, 1, 64);
+        hb[0] = odd ? o0 : h0;
+        hb[1] = odd ? o1 : h1;
+        hb[2] = odd ? h0 : o0;
+        hb[3] = odd ? h1 : o1;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = wm * WM + i * 16 + fq * 4 + e;
-        Cs[row * CLD + col] = (T)(acc[i][j][e] * alpha + bv);
+        float v = acc[i][j][e] * alpha + bv;
+        if (ext_masked) {
+          const uint32_t bits = (N & 1) ? mift_bits16(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col)
+                                        : ((hb[e] >> ((col & 1) << 4)) & 0xFFFFu);
+          v += bits >= ep.ext_thr ? xt[e] * ep.ext_inv_keep : 0.f;
+        }
+        Cs[row * CLD + col] = (T)v;
       }
     }
   }
@@ -306,7 +339,8 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                         const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& residual,
                         double dropout_p, int64_t seed, bool want_preact, double alpha,
                         const c10::optional<at::Tensor>& out, int64_t tile,
-                        const c10::optional<at::Tensor>& alpha_t, const c10::optional<at::Tensor>& pre_add) {
+                        const c10::optional<at::Tensor>& alpha_t, const c10::optional<at::Tensor>& pre_add,
+                        double ext_p, int64_t ext_seed) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm_nt: GPU tensors required");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_nt: 2-D operands");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_nt: K must be contiguous");
@@ -358,6 +392,9 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     TORCH_CHECK(alpha_t->scalar_type() == at::kFloat && alpha_t->is_cuda(), "gemm_nt: alpha_t fp32 GPU");
     ep.alpha_ptr = alpha_t->data_ptr<float>();
   }
+  ep.ext_thr = mift_thr16(ext_p);
+  ep.ext_seed = (uint64_t)ext_seed;
+  ep.ext_inv_keep = ext_p > 0 ? mift_inv_keep(ext_p) : 1.f;
   ep.pre_add = nullptr;
   if (pre_add) {
     TORCH_CHECK(pre_add->size(0) == M && pre_add->size(1) == N && pre_add->stride(0) == c.stride(0) &&

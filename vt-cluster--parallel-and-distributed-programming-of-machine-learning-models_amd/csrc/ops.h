@@ -18,7 +18,14 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                                      const c10::optional<at::Tensor>& residual, double dropout_p, int64_t seed,
                                      bool want_preact, double alpha, const c10::optional<at::Tensor>& out,
                                      int64_t tile, const c10::optional<at::Tensor>& alpha_t,
-                                     const c10::optional<at::Tensor>& pre_add);
+                                     const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed);
+
+// ---- LoRA side path (kernels/lora.hip)
+at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed);
+void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, double p, int64_t seed, int64_t mode,
+                     int64_t rank, int64_t offset);
+void mift_pack_lora_all(const at::Tensor& arena, const at::Tensor& table, const at::Tensor& scales, at::Tensor& out,
+                        int64_t max_elems);
 
 // ---- elementwise / embedding / LoRA pack (kernels/elementwise.hip)
 at::Tensor mift_mask_scale(const at::Tensor& x, double p, int64_t seed, const c10::optional<at::Tensor>& out,
@@ -48,6 +55,9 @@ at::Tensor mift_attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at
                          const c10::optional<at::Tensor>& kv_len);
 
 #define MIFT_BIND_MORE(m) \
+  m.def("lora_proj", &mift_lora_proj, "out[M,32] = alpha*drop(x)@w^T (tall-skinny MFMA)"); \
+  m.def("lora_wgrad", &mift_lora_wgrad, "out[P,32] += drop(x)^T @ y (tr_b16 split-M MFMA); arena modes"); \
+  m.def("pack_lora_all", &mift_pack_lora_all, "pack every adapter's 16-bit operands from the fp32 arena"); \
   m.def("attn_fwd", &mift_attn_fwd, "causal flash attention fwd on fused qkv -> (o, lse)"); \
   m.def("attn_bwd", &mift_attn_bwd, "causal flash attention bwd -> dqkv"); \
   m.def("gemm_nt", &mift_gemm_nt, "C = epi(A @ B^T [+ A2 @ B2^T]) MFMA bf16/fp16"); \

@@ -115,9 +115,22 @@ class LoraArena:
             p.data = view
             p.grad = self.grad[o:o + p.numel()].view_as(p)
         self.model = model
+        self.version = 0  # bumped whenever the parameters change (optimizer step, load)
+        # bind every adapted Linear to its arena slices (fused path writes grads in place)
+        off_of = {id(p): o for (_, p), o in zip(self.named, self.offsets)}
+        self.modules = []
+        for _, m in model.named_modules():
+            if isinstance(m, Linear) and m.lora_r > 0 and id(m.lora_A.weight) in off_of:
+                m._arena = self
+                m._offA = off_of[id(m.lora_A.weight)]
+                m._offB = off_of[id(m.lora_B.weight)]
+                self.modules.append(m)
 
     def zero_grad(self):
         self.grad.zero_()
+
+    def bump(self):
+        self.version += 1
 
     def rebind_grads(self):
         """Re-point .grad to the arena (autograd may have replaced it)."""

@@ -10,11 +10,34 @@ ACT_BWD = {0: 0, 1: 4, 2: 5, 3: 6}
 
 
 def gemm(a, b, bias=None, a2=None, b2=None, act=0, aux=None, residual=None, dropout_p=0.0, seed=0,
-         want_preact=False, alpha=1.0, out=None, tile=0, alpha_t=None, pre_add=None):
-    """out = epi(a @ b.T [+ a2 @ b2.T]); see csrc/kernels/gemm.hip."""
+         want_preact=False, alpha=1.0, out=None, tile=0, alpha_t=None, pre_add=None, ext_p=0.0, ext_seed=0):
+    """out = epi(a @ b.T [+ a2 @ b2.T]); see csrc/kernels/gemm.hip.
+
+    ``ext_p > 0`` keeps the a2·b2ᵀ K-extension separate and adds it under the
+    dropout mask (ext_seed, ext_p) — the LoRA input-dropout backward."""
     y, pre = C().gemm_nt(a, b, bias, a2, b2, int(act), aux, residual, float(dropout_p), int(seed),
-                         bool(want_preact), float(alpha), out, int(tile), alpha_t, pre_add)
+                         bool(want_preact), float(alpha), out, int(tile), alpha_t, pre_add, float(ext_p),
+                         int(ext_seed))
     return (y, pre) if want_preact else y
+
+
+def lora_proj(x, w32, alpha=1.0, p=0.0, seed=0):
+    """[M,32] = alpha * dropout(x) @ w32.T   (w32: [32, K])."""
+    return C().lora_proj(x, w32, float(alpha), float(p), int(seed))
+
+
+def lora_wgrad(x, y32, out=None, p=0.0, seed=0):
+    """out[P,32] (fp32) += dropout(x).T @ y32."""
+    import torch
+    if out is None:
+        out = torch.zeros(x.shape[1], 32, dtype=torch.float32, device=x.device)
+    C().lora_wgrad(x, y32, out, float(p), int(seed), 0, 32, 0)
+    return out
+
+
+def lora_wgrad_into(x, y32, arena_grad, mode, rank, offset, p=0.0, seed=0):
+    """Accumulate dropout(x).T @ y32 into a flat fp32 arena: mode 1 -> [P, rank] (dB), 2 -> [rank, P] (dA)."""
+    C().lora_wgrad(x, y32, arena_grad, float(p), int(seed), int(mode), int(rank), int(offset))
 
 
 def layer_norm_fwd(x, w, b, eps):

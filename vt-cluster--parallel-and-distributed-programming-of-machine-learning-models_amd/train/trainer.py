@@ -66,6 +66,11 @@ class Trainer:
         self.dp_group = ctx.dp_group if ctx else None
         self.dp = ctx.dp if ctx else 1
         self.arena = LoraArena(model, device=self.device)
+        if self.device.type == "cuda" and getattr(model, "fused", False):
+            from ..lora.pack import attach
+            from ..ops.dispatch import use_kernels
+            if use_kernels(self.arena.param):
+                attach(model, self.arena, next(p for n, p in model.named_parameters() if "lora_" not in n).dtype)
         self.reducer = GradReducer(self.arena, group=self.dp_group, bucket_mb=cfg.bucket_mb, world=self.dp)
         self.opt = FusedAdamW(self.arena.param, self.arena.grad, lr=cfg.lr, weight_decay=cfg.weight_decay,
                               max_grad_norm=cfg.max_grad_norm,
@@ -135,6 +140,7 @@ class Trainer:
         self.arena.rebind_grads()
         self.reducer.finish()
         self.opt.step()
+        self.arena.bump()
         self.global_step += 1
         return loss_acc, ntok
 
@@ -231,6 +237,7 @@ class Trainer:
         self.global_step = st["global_step"]
         self.history = st.get("log_history", [])
         self.model.micro_step = st.get("micro_step", 0)
+        self.arena.bump()
         rp = os.path.join(path, f"rng_state_{self.rank}.pth")
         if os.path.exists(rp):
             torch.set_rng_state(torch.load(rp, weights_only=True)["cpu"])
