@@ -163,6 +163,50 @@ MIFT_HD void store8(T* p, const float* in) {
   }
 }
 
+// 4 elements (8 B for 16-bit types).
+template <typename T>
+MIFT_HD void load4(const T* p, float* out) {
+  if constexpr (sizeof(T) == 4) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+  } else {
+    short4_ v = *reinterpret_cast<const short4_*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      short s = v[i];
+      T t;
+      __builtin_memcpy(&t, &s, 2);
+      out[i] = (float)t;
+    }
+  }
+}
+template <typename T>
+MIFT_HD void store4(T* p, const float* in) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(in[0], in[1], in[2], in[3]);
+  } else {
+    short4_ v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      T t = (T)in[i];
+      short s;
+      __builtin_memcpy(&s, &t, 2);
+      v[i] = s;
+    }
+    *reinterpret_cast<short4_*>(p) = v;
+  }
+}
+MIFT_HD void mift_keep4(uint64_t seed, uint64_t idx0, uint32_t thr, bool* k) {
+  if ((idx0 & 1) == 0) {
+    const uint32_t h0 = mift_hash_pair(seed, idx0 >> 1), h1 = mift_hash_pair(seed, (idx0 >> 1) + 1);
+    k[0] = (h0 & 0xFFFFu) >= thr; k[1] = (h0 >> 16) >= thr;
+    k[2] = (h1 & 0xFFFFu) >= thr; k[3] = (h1 >> 16) >= thr;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) k[e] = mift_keep(seed, idx0 + e, thr);
+  }
+}
+
 #define MIFT_CHECK_HIP(expr)                                                        \
   do {                                                                              \
     hipError_t _e = (expr);                                                         \

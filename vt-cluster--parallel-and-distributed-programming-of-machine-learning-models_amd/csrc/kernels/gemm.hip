@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(af[i], bfv[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(bfv[j], af[i], acc[i][j]);
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -208,58 +208,52 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(af2[i], bf2[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(bf2[j], af2[i], acc[i][j]);
     }
   }
   const bool ext_masked = ext && ep.ext_thr != 0;
 
-  // ---- epilogue phase 1: acc (*alpha, +bias) -> T tile in LDS [BM][BN] ----
+  // ---- epilogue phase 1: accumulators (*alpha, +bias, +masked LoRA ext) -> LDS tile ----
+  // MFMA operands are swapped (A-slot = B tile, B-slot = A tile), so the
+  // accumulator of tile (i,j) holds C[row = .. + fr][col = .. + 4*fq + e]:
+  // four CONSECUTIVE columns per lane -> one 8-byte ds_write per tile and two
+  // pair-hashes per four dropout decisions.
+  __syncthreads();  // staging buffers are reused for the C tile
   T* Cs = reinterpret_cast<T*>(smem);
-  constexpr int CLD = BN + 8;  // padded row (elements) to spread banks
+  constexpr int CLD = BN + 8;
   const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = wn * WN + j * 16 + fr;
-    float bv = 0.f;
-    if (ep.bias != nullptr && n0 + col < N)
-      bv = ep.bias_f32 ? reinterpret_cast<const float*>(ep.bias)[n0 + col]
-                       : (float)reinterpret_cast<const T*>(ep.bias)[n0 + col];
+    const int col = wn * WN + j * 16 + fq * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ep.bias != nullptr && n0 + col < N) {
+      if (ep.bias_f32) {
+        float4 t4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ep.bias) + n0 + col);
+        bv[0] = t4.x; bv[1] = t4.y; bv[2] = t4.z; bv[3] = t4.w;
+      } else {
+        load4<T>(reinterpret_cast<const T*>(ep.bias) + n0 + col, bv);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      float4_ xt = float4_{0.f, 0.f, 0.f, 0.f};
-      uint32_t hb[4] = {0, 0, 0, 0};
-      if (ext_masked) {
-        xt = mfma16<T>(af2[i], bf2[j], xt);
-        // lanes fr and fr^1 hold columns (2c, 2c+1) = one hash pair per row:
-        // the even lane hashes rows e=0,1, the odd lane rows e=2,3, then swap.
-        const int rbase = m0 + wm * WM + i * 16 + fq * 4;
-        const int odd = fr & 1;
-        const uint64_t p0 = ((uint64_t)(rbase + 2 * odd) * N + n0 + col) >> 1;
-        const uint64_t p1 = ((uint64_t)(rbase + 2 * odd + 1) * N + n0 + col) >> 1;
-        const uint32_t h0 = mift_hash_pair(ep.ext_seed, p0), h1 = mift_hash_pair(ep.ext_seed, p1);
-        const uint32_t o0 = __shfl_xor(h0, 1, 64), o1 = __shfl_xor(h1, 1, 64);
-        hb[0] = odd ? o0 : h0;
-        hb[1] = odd ? o1 : h1;
-        hb[2] = odd ? h0 : o0;
-        hb[3] = odd ? h1 : o1;
-      }
+      const int row = wm * WM + i * 16 + fr;
+      float z[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wm * WM + i * 16 + fq * 4 + e;
-        float v = acc[i][j][e] * alpha + bv;
-        if (ext_masked) {
-          const uint32_t bits = (N & 1) ? mift_bits16(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col)
-                                        : ((hb[e] >> ((col & 1) << 4)) & 0xFFFFu);
-          v += bits >= ep.ext_thr ? xt[e] * ep.ext_inv_keep : 0.f;
-        }
-        Cs[row * CLD + col] = (T)v;
+      for (int e = 0; e < 4; ++e) z[e] = acc[i][j][e] * alpha + bv[e];
+      if (ext_masked) {
+        float4_ xt = mfma16<T>(bf2[j], af2[i], float4_{0.f, 0.f, 0.f, 0.f});
+        bool kp[4];
+        mift_keep4(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col, ep.ext_thr, kp);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[e] += kp[e] ? xt[e] * ep.ext_inv_keep : 0.f;
       }
+      store4<T>(Cs + row * CLD + col, z);
     }
   }
   __syncthreads();
 
-  // ---- epilogue phase 2: 8 columns per thread, 16-B vector I/O ----
-  constexpr int VPR = BN / 8;  // vectors per row
+  // ---- epilogue phase 2: 8 columns per thread, 16-B vector I/O, whole rows ----
+  constexpr int VPR = BN / 8;
   for (int v = tid; v < BM * VPR; v += 256) {
     const int row = v / VPR, c8 = (v % VPR) * 8;
     const int gr = m0 + row, gc = n0 + c8;
@@ -348,6 +342,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
   const int M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K, "gemm_nt: K mismatch");
   TORCH_CHECK(K % 64 == 0, "gemm_nt: K must be a multiple of 64, got ", K);
+  TORCH_CHECK(N % 4 == 0, "gemm_nt: N must be a multiple of 4, got ", N);
   TORCH_CHECK((a.stride(0) % 8) == 0 && (b.stride(0) % 8) == 0, "gemm_nt: row strides must be 16-B aligned");
   at::Tensor c = out ? *out : at::empty({M, N}, a.options());
   TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.stride(0) % 8 == 0, "gemm_nt: bad out");
