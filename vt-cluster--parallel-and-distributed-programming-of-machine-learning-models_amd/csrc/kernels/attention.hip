@@ -3,23 +3,26 @@
 // Layout: the fused projection output qkv [B*S, 3*H*HD] (token-major, as the
 // qkv GEMM writes it) is read in place — no head split / transpose kernels.
 // Output o [B*S, H*HD]; lse [B, H, S] fp32 (natural log of the softmax
-// denominator of scale*QK^T) for the backward.  Head dims 64 (GPT-2),
+// denominator of scale*QK^T) for the backward.  Head dims 32, 64 (GPT-2),
 // 80 (OPT-2.7B; QK^T K-steps zero-padded to 96) and 128 (OPT-6.7B).
 //
 // MFMA mapping (16x16x32 bf16, "swapped" products, guide §3):
-//   forward  S^T[key, q] = K · Q^T   A = K rows (LDS), B = Q rows (registers)
-//            -> each lane owns ONE query (lane & 15) and 4 keys per 16-key
-//               sub-tile, so the P tile is already the A operand of P·V up to
-//               a k-permutation; V is staged transposed + key-permuted in LDS
-//               so the matching B fragment is one 16-B ds_read (no P round
-//               trip through LDS, no cross-lane shuffles for P).
-//   Online softmax in exp2 with per-query running max/sum; O rescale factors
-//   are moved to the accumulator layout with 4 shuffles per KV tile.
-// Backward (FA2 split, no atomics): attn_bwd_dq (mirror of the forward: Q,
-// dO in registers, loop over key tiles, dQ += dS·K) and attn_bwd_dkdv (one
-// key tile per block, loop over query tiles, S = Q·K^T in the lane-per-key
-// layout, dV += P^T dO and dK += dS^T Q with transposed/permuted dO^T, Q^T
-// images in LDS).  D = rowsum(dO ∘ O) comes from attn_bwd_pre.
+//   forward  S^T[key, q] = K · Q^T   A = K rows (LDS, ds_read_b128),
+//            B = Q rows (registers) -> each lane owns ONE query (lane & 15)
+//            and 4 keys per 16-key sub-tile, so the P tile already is the A
+//            operand of P·V up to a k-permutation (keys 4g..4g+3 and
+//            16+4g..16+4g+3 of each 32-key step).  The matching V^T fragment
+//            is two gfx950 hardware-transpose reads (ds_read_b64_tr_b16,
+//            guide T10) of the row-major V tile: no transposed LDS writes, no
+//            P round trip, no cross-lane shuffles for P.
+//   Tiles stream through registers: tile t+1's K/V global loads are issued
+//   before tile t's MFMAs (T14 issue-early / write-late).
+//   LDS row strides: b128-read images use HDP*2+16 B, tr-read images an odd
+//   multiple of 32 B, so both access kinds are bank-conflict free.
+// Backward (FA2 split, no atomics): attn_bwd_dq (mirror of the forward, also
+// computes D = rowsum(dO∘O) for its queries) then attn_bwd_dkdv (one key tile
+// per block, loop over query tiles; S = Q·K^T in the lane-per-key layout,
+// dV += P^T dO and dK += dS^T Q with tr-read B operands).
 // Dropout (GPT-2 attn_pdrop 0.1): counter hash of idx = ((b*H+h)*S+q)*S+k,
 // identical in all kernels (see common.h).
 #include "common.h"
@@ -32,16 +35,10 @@ constexpr int BQ = 64, BKV = 64;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
+typedef short v4s __attribute__((ext_vector_type(4)));
+
 MIFT_HD float4_ mfma_bf16(bf16x8 a, bf16x8 b, float4_ c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// key position inside a 64-key "permuted" row so that the 8 keys a lane group
-// g contributes to K-step s2 of the P·V product are contiguous:
-//   key = 32*s2 + 16*t + 4*g + r  ->  pos = 32*s2 + 8*g + 4*t + r
-MIFT_HD int perm_pos(int key) {
-  const int s2 = key >> 5, t = (key >> 4) & 1, g = (key >> 2) & 3, r = key & 3;
-  return (s2 << 5) | (g << 3) | (t << 2) | r;
 }
 
 template <int HD>
@@ -49,11 +46,13 @@ struct Geo {
   static constexpr int HDP = (HD + 31) / 32 * 32;  // padded for 32-deep K steps
   static constexpr int NKS = HDP / 32;             // K-steps over head dim
   static constexpr int NOT = HD / 16;              // 16-wide output tiles
-  static constexpr int RS = HDP * 2 + 16;          // row-tile stride (bytes)
-  static constexpr int CS = BKV * 2 + 16;          // col-tile stride (bytes)
+  static constexpr int RS = HDP * 2 + 16;          // b128-read image stride (bytes)
+  static constexpr int TS = ((HD * 2 + 31) / 32) | 1;  // tr-read image stride / 32 (odd)
+  static constexpr int TRS = TS * 32;
   static constexpr int ROW_BYTES = 64 * RS;
-  static constexpr int COL_BYTES = HD * CS;
+  static constexpr int TR_BYTES = 64 * TRS;
   static constexpr int CH = HD / 8;                // 16-B chunks per row
+  static constexpr int NCH = (64 * CH + 255) / 256;  // chunks per thread per 64-row tile
 };
 
 MIFT_HD bf16x8 ld_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -65,32 +64,47 @@ MIFT_HD bf16x8 zero_frag() {
   return z;
 }
 
-// Load a 64-row x HD tile (rows row0.., clamped to [0,nrows)) from a strided
-// bf16 matrix into a row tile (stride RS, padded columns zeroed once by caller).
-template <int HD>
-MIFT_HD void load_row_tile(char* dst, const bf16* src, int64_t ld, int row0, int nrows, int tid) {
-  using G = Geo<HD>;
-  for (int i = tid; i < 64 * G::CH; i += 256) {
-    const int r = i / G::CH, c = i % G::CH;
-    const int gr = min(row0 + r, nrows - 1);
-    short8 v = *reinterpret_cast<const short8*>(src + (int64_t)gr * ld + c * 8);
-    *reinterpret_cast<short8*>(dst + r * G::RS + c * 16) = v;
-  }
+// B fragment from a row-major [key][hd] image by two transpose reads:
+// lane (li, g) gets X[kbase + 4g + 0..3][col0 + li] and X[kbase + 16 + 4g + 0..3][col0 + li]
+MIFT_HD bf16x8 tr_frag(const char* img, int stride, int kbase, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int off = (kbase + 4 * g + (li >> 2)) * stride + (col0 + (li & 3) * 4) * 2;
+  v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + off));
+  v4s b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + off + 16 * stride));
+  short8 t = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  bf16x8 f;
+  __builtin_memcpy(&f, &t, 16);
+  return f;
 }
 
-// Same source, written transposed + key-permuted: dst[hd][perm_pos(row)].
+// register-staged 64-row tile: global -> regs (issue early) -> LDS image(s) (write late)
 template <int HD>
-MIFT_HD void load_col_tile(char* dst, const bf16* src, int64_t ld, int row0, int nrows, int tid) {
-  using G = Geo<HD>;
-  for (int i = tid; i < 64 * G::CH; i += 256) {
-    const int r = i % 64, c = i / 64;
-    const int gr = min(row0 + r, nrows - 1);
-    short8 v = *reinterpret_cast<const short8*>(src + (int64_t)gr * ld + c * 8);
-    const int pos = perm_pos(r);
+struct TileRegs {
+  short8 v[Geo<HD>::NCH];
+  MIFT_HD void load(const bf16* src, int64_t ld, int row0, int nrows, int tid) {
+    using G = Geo<HD>;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) *reinterpret_cast<short*>(dst + (c * 8 + e) * G::CS + pos * 2) = v[e];
+    for (int k = 0; k < G::NCH; ++k) {
+      const int i = tid + k * 256;
+      if (i < 64 * G::CH) {
+        const int r = i / G::CH, c = i % G::CH;
+        const int gr = min(row0 + r, nrows - 1);
+        v[k] = *reinterpret_cast<const short8*>(src + (int64_t)gr * ld + c * 8);
+      }
+    }
   }
-}
+  MIFT_HD void store(char* img, int stride, int tid) const {
+    using G = Geo<HD>;
+#pragma unroll
+    for (int k = 0; k < G::NCH; ++k) {
+      const int i = tid + k * 256;
+      if (i < 64 * G::CH) {
+        const int r = i / G::CH, c = i % G::CH;
+        *reinterpret_cast<short8*>(img + r * stride + c * 16) = v[k];
+      }
+    }
+  }
+};
 
 template <int HD>
 MIFT_HD void zero_row_pad(char* dst, int tid) {
@@ -103,7 +117,7 @@ MIFT_HD void zero_row_pad(char* dst, int tid) {
   }
 }
 
-// Q-style fragments for 16 rows straight from global: frag[s] = X[row0 + (lane&15)][32s + 8(lane>>4) ..]
+// fragments for 16 rows straight from global: frag[s] = X[row][32s + 8(lane>>4) ..]
 template <int HD>
 MIFT_HD void load_reg_frags(bf16x8* f, const bf16* src, int64_t ld, int row, int nrows, int lane) {
   using G = Geo<HD>;
@@ -127,8 +141,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
                                                        uint32_t thr, float inv_keep) {
   using G = Geo<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Ks = smem;
-  char* Vt = smem + G::ROW_BYTES;
+  char* Ks = smem;                    // [64][HDP] b128 image
+  char* Vs = smem + G::ROW_BYTES;     // [64][HD] tr image
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, qc = lane & 15;
   const int nqt = (S + BQ - 1) / BQ;
@@ -156,32 +170,40 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 
   const int kend = min((qt + 1) * BQ, klen);
   const int nkt = (kend + BKV - 1) / BKV;
+  TileRegs<HD> kr, vr;
+  if (nkt > 0) {
+    kr.load(Kg, ld, 0, S, tid);
+    vr.load(Vg, ld, 0, S, tid);
+  }
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * BKV;
     __syncthreads();
-    load_row_tile<HD>(Ks, Kg, ld, k0, S, tid);
-    load_col_tile<HD>(Vt, Vg, ld, k0, S, tid);
+    kr.store(Ks, G::RS, tid);
+    vr.store(Vs, G::TRS, tid);
     __syncthreads();
-    // S^T tile: 4 sub-tiles of 16 keys
+    if (kt + 1 < nkt) {  // next tile in flight during this tile's math
+      kr.load(Kg, ld, k0 + BKV, S, tid);
+      vr.load(Vg, ld, k0 + BKV, S, tid);
+    }
     float4_ st[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       st[t] = float4_{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < G::NKS; ++s) {
-        bf16x8 kf = ld_frag(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16);
-        st[t] = mfma_bf16(kf, qf[s], st[t]);
-      }
+      for (int s = 0; s < G::NKS; ++s)
+        st[t] = mfma_bf16(ld_frag(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], st[t]);
     }
-    // mask + tile max (per query: lane-local 16 values, then across the 4 groups)
+    const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
     float tmax = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = k0 + t * 16 + g * 4 + r;
         float v = st[t][r] * c2;
-        if (key > myq || key >= klen) v = -INFINITY;
+        if (diag) {
+          const int key = k0 + t * 16 + g * 4 + r;
+          if (key > myq || key >= klen) v = -INFINITY;
+        }
         st[t][r] = v;
         tmax = fmaxf(tmax, v);
       }
@@ -198,30 +220,21 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
       for (int r = 0; r < 4; ++r) {
         float p = (mnew == -INFINITY) ? 0.f : exp2f(st[t][r] - mnew);
         psum += p;
-        if (thr != 0) {
-          const int key = k0 + t * 16 + g * 4 + r;
-          p = drop_keep(seed, thr, bh, S, myq, key) ? p * inv_keep : 0.f;
-        }
+        if (thr != 0) p = drop_keep(seed, thr, bh, S, myq, k0 + t * 16 + g * 4 + r) ? p * inv_keep : 0.f;
         pf[t >> 1][(t & 1) * 4 + r] = (bf16)p;
       }
     l = l * alpha + psum;
-    // rescale O (acc layout: row = g*4 + r -> query q0 + g*4 + r lives in lane g*4+r)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float ar = __shfl(alpha, g * 4 + r, 64);
 #pragma unroll
       for (int i = 0; i < G::NOT; ++i) o[i][r] *= ar;
     }
-    // O += P · V
 #pragma unroll
     for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 vf = ld_frag(Vt + (i * 16 + qc) * G::CS + (32 * s2 + 8 * g) * 2);
-        o[i] = mfma_bf16(pf[s2], vf, o[i]);
-      }
+      for (int s2 = 0; s2 < 2; ++s2) o[i] = mfma_bf16(pf[s2], tr_frag(Vs, G::TRS, 32 * s2, i * 16, lane), o[i]);
   }
-  // finalize
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   const float inv_l = l > 0.f ? 1.f / l : 0.f;
@@ -238,38 +251,18 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   }
 }
 
-// ======================== backward: D = rowsum(dO∘O) ========================
+// ============================ backward: dQ (+D) =============================
 template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
-                                                           float* __restrict__ Dv, int BS, int H, int S) {
-  // one wave per (token, head)
-  const int lane = threadIdx.x & 63;
-  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (item >= (int64_t)BS * H) return;
-  const int64_t tok = item / H;
-  const int h = item % H;
-  const int D = H * HD;
-  float s = 0.f;
-  for (int c = lane; c < HD; c += 64) s += (float)o[tok * D + h * HD + c] * (float)dout[tok * D + h * HD + c];
-  s = wave_sum(s);
-  if (lane == 0) {
-    const int b = tok / S, q = tok % S;
-    Dv[((int64_t)b * H + h) * S + q] = s;
-  }
-}
-
-// ============================ backward: dQ =================================
-template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                          const float* __restrict__ lse, const float* __restrict__ Dv,
-                                                          bf16* __restrict__ dqkv, const int* __restrict__ kv_len,
-                                                          int B, int S, int H, float scale, uint64_t seed,
-                                                          uint32_t thr, float inv_keep) {
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o,
+                                                          const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                          float* __restrict__ Dv, bf16* __restrict__ dqkv,
+                                                          const int* __restrict__ kv_len, int B, int S, int H,
+                                                          float scale, uint64_t seed, uint32_t thr, float inv_keep) {
   using G = Geo<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Ks = smem;                       // K rows (A of S^T)
-  char* Vs = smem + G::ROW_BYTES;        // V rows (A of dP^T)
-  char* Kt = smem + 2 * G::ROW_BYTES;    // K^T permuted (B of dQ)
+  char* Ks = smem;                                 // K rows, b128 image (A of S^T)
+  char* Vs = smem + G::ROW_BYTES;                  // V rows, b128 image (A of dP^T)
+  char* Kt = smem + 2 * G::ROW_BYTES;              // K rows, tr image (B of dQ)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, qc = lane & 15;
   const int nqt = (S + BQ - 1) / BQ;
@@ -282,6 +275,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const bf16* Kg = Qg + D;
   const bf16* Vg = Qg + 2 * D;
   const bf16* dOg = dout + (int64_t)b * S * D + h * HD;
+  const bf16* Og = o + (int64_t)b * S * D + h * HD;
   const int klen = kv_len ? kv_len[b] : S;
   const int q0 = qt * BQ + wave * 16;
   const int myq = q0 + qc;
@@ -290,8 +284,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   bf16x8 qf[G::NKS], df[G::NKS];
   load_reg_frags<HD>(qf, Qg, ld, myq, S, lane);
   load_reg_frags<HD>(df, dOg, D, myq, S, lane);
+  // D = rowsum(dO ∘ O) for this lane's query (fused attn_bwd_pre)
+  float Dq = 0.f;
+  {
+    bf16x8 of[G::NKS];
+    load_reg_frags<HD>(of, Og, D, myq, S, lane);
+#pragma unroll
+    for (int s = 0; s < G::NKS; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Dq += (float)of[s][e] * (float)df[s][e];
+    Dq += __shfl_xor(Dq, 16, 64);
+    Dq += __shfl_xor(Dq, 32, 64);
+    if (g == 0 && myq < S) Dv[(int64_t)bh * S + myq] = Dq;
+  }
   const float lse2 = myq < S ? lse[(int64_t)bh * S + myq] * LOG2E : 0.f;
-  const float Dq = myq < S ? Dv[(int64_t)bh * S + myq] : 0.f;
   zero_row_pad<HD>(Ks, tid);
   zero_row_pad<HD>(Vs, tid);
 
@@ -301,13 +307,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 
   const int kend = min((qt + 1) * BQ, klen);
   const int nkt = (kend + BKV - 1) / BKV;
+  TileRegs<HD> kr, vr;
+  if (nkt > 0) {
+    kr.load(Kg, ld, 0, S, tid);
+    vr.load(Vg, ld, 0, S, tid);
+  }
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * BKV;
     __syncthreads();
-    load_row_tile<HD>(Ks, Kg, ld, k0, S, tid);
-    load_row_tile<HD>(Vs, Vg, ld, k0, S, tid);
-    load_col_tile<HD>(Kt, Kg, ld, k0, S, tid);
+    kr.store(Ks, G::RS, tid);
+    kr.store(Kt, G::TRS, tid);
+    vr.store(Vs, G::RS, tid);
     __syncthreads();
+    if (kt + 1 < nkt) {
+      kr.load(Kg, ld, k0 + BKV, S, tid);
+      vr.load(Vg, ld, k0 + BKV, S, tid);
+    }
     bf16x8 dsf[2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -320,18 +335,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + t * 16 + g * 4 + r;
-        float p = (key > myq || key >= klen) ? 0.f : exp2f(sa[r] * c2 - lse2);
+        const float p = (key > myq || key >= klen) ? 0.f : exp2f(sa[r] * c2 - lse2);
         float dp = pa[r];
         if (thr != 0) dp = drop_keep(seed, thr, bh, S, myq, key) ? dp * inv_keep : 0.f;
-        const float ds = p * (dp - Dq);
-        dsf[t >> 1][(t & 1) * 4 + r] = (bf16)ds;
+        dsf[t >> 1][(t & 1) * 4 + r] = (bf16)(p * (dp - Dq));
       }
     }
 #pragma unroll
     for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        dq[i] = mfma_bf16(dsf[s2], ld_frag(Kt + (i * 16 + qc) * G::CS + (32 * s2 + 8 * g) * 2), dq[i]);
+      for (int s2 = 0; s2 < 2; ++s2) dq[i] = mfma_bf16(dsf[s2], tr_frag(Kt, G::TRS, 32 * s2, i * 16, lane), dq[i]);
   }
   bf16* dQg = dqkv + (int64_t)b * S * ld + h * HD;
 #pragma unroll
@@ -353,11 +366,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
                                                             uint32_t thr, float inv_keep) {
   using G = Geo<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Qs = smem;                                   // Q rows (A of S)
-  char* dOs = smem + G::ROW_BYTES;                   // dO rows (A of dP)
-  char* Qt = smem + 2 * G::ROW_BYTES;                // Q^T permuted (B of dK)
-  char* dOt = Qt + G::COL_BYTES;                     // dO^T permuted (B of dV)
-  float* lse_s = reinterpret_cast<float*>(dOt + G::COL_BYTES);
+  char* Qs = smem;                                   // Q rows b128 image (A of S)
+  char* dOs = smem + G::ROW_BYTES;                   // dO rows b128 image (A of dP)
+  char* Qt = smem + 2 * G::ROW_BYTES;                // Q rows tr image (B of dK)
+  char* dOt = Qt + G::TR_BYTES;                      // dO rows tr image (B of dV)
+  float* lse_s = reinterpret_cast<float*>(dOt + G::TR_BYTES);
   float* D_s = lse_s + 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, kc = lane & 15;
@@ -376,7 +389,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
   const int mykey = k0 + kc;
   const float c2 = scale * LOG2E;
 
-  // K, V fragments of this wave's 16 keys as B operands: B[k=hd][n=key] = X[key][hd]
   bf16x8 kf[G::NKS], vf[G::NKS];
   load_reg_frags<HD>(kf, Kg, ld, mykey, S, lane);
   load_reg_frags<HD>(vf, Vg, ld, mykey, S, lane);
@@ -391,19 +403,29 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
   }
   const int nqt = (S + BQ - 1) / BQ;
   const bool active = kt * BKV < klen;
-  for (int qt = active ? kt : nqt; qt < nqt; ++qt) {
+  const int qt0 = active ? kt : nqt;
+  TileRegs<HD> qr, dr;
+  if (qt0 < nqt) {
+    qr.load(Qg, ld, qt0 * BQ, S, tid);
+    dr.load(dOg, D, qt0 * BQ, S, tid);
+  }
+  for (int qt = qt0; qt < nqt; ++qt) {
     const int qb = qt * BQ;
     __syncthreads();
-    load_row_tile<HD>(Qs, Qg, ld, qb, S, tid);
-    load_row_tile<HD>(dOs, dOg, D, qb, S, tid);
-    load_col_tile<HD>(Qt, Qg, ld, qb, S, tid);
-    load_col_tile<HD>(dOt, dOg, D, qb, S, tid);
+    qr.store(Qs, G::RS, tid);
+    qr.store(Qt, G::TRS, tid);
+    dr.store(dOs, G::RS, tid);
+    dr.store(dOt, G::TRS, tid);
     if (tid < 64) {
       const int q = min(qb + tid, S - 1);
       lse_s[tid] = lse[(int64_t)bh * S + q] * LOG2E;
       D_s[tid] = Dv[(int64_t)bh * S + q];
     }
     __syncthreads();
+    if (qt + 1 < nqt) {
+      qr.load(Qg, ld, qb + BQ, S, tid);
+      dr.load(dOg, D, qb + BQ, S, tid);
+    }
     bf16x8 pf[2], dsf[2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -426,17 +448,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
           pd = kp ? p * inv_keep : 0.f;
           dp = kp ? dp * inv_keep : 0.f;
         }
-        const float ds = p * (dp - D_s[ql]);
         pf[t >> 1][(t & 1) * 4 + r] = (bf16)pd;
-        dsf[t >> 1][(t & 1) * 4 + r] = (bf16)ds;
+        dsf[t >> 1][(t & 1) * 4 + r] = (bf16)(p * (dp - D_s[ql]));
       }
     }
 #pragma unroll
     for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        dv[i] = mfma_bf16(pf[s2], ld_frag(dOt + (i * 16 + kc) * G::CS + (32 * s2 + 8 * g) * 2), dv[i]);
-        dk[i] = mfma_bf16(dsf[s2], ld_frag(Qt + (i * 16 + kc) * G::CS + (32 * s2 + 8 * g) * 2), dk[i]);
+        dv[i] = mfma_bf16(pf[s2], tr_frag(dOt, G::TRS, 32 * s2, i * 16, lane), dv[i]);
+        dk[i] = mfma_bf16(dsf[s2], tr_frag(Qt, G::TRS, 32 * s2, i * 16, lane), dk[i]);
       }
   }
   bf16* dKg = dqkv + (int64_t)b * S * ld + D + h * HD;
@@ -454,14 +475,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
   }
 }
 
-uint32_t thr_of(double p) { return mift_thr16(p); }
-
 template <int HD>
 void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int* kvl, int B, int S, int H, float scale,
                 uint64_t seed, uint32_t thr, float inv_keep, hipStream_t st) {
   using G = Geo<HD>;
   const int nqt = (S + BQ - 1) / BQ;
-  const int smem = G::ROW_BYTES + G::COL_BYTES;
+  const int smem = G::ROW_BYTES + G::TR_BYTES;
   hipLaunchKernelGGL((attn_fwd_kernel<HD>), dim3(B * H * nqt), dim3(256), smem, st, (const bf16*)qkv.data_ptr(),
                      (bf16*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, thr, inv_keep);
 }
@@ -471,15 +490,12 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
                 at::Tensor& Dv, at::Tensor& dqkv, const int* kvl, int B, int S, int H, float scale, uint64_t seed,
                 uint32_t thr, float inv_keep, hipStream_t st) {
   using G = Geo<HD>;
-  const int BS = B * S;
-  hipLaunchKernelGGL((attn_bwd_pre_kernel<HD>), dim3(((int64_t)BS * H + 3) / 4), dim3(256), 0, st,
-                     (const bf16*)o.data_ptr(), (const bf16*)dout.data_ptr(), Dv.data_ptr<float>(), BS, H, S);
   const int nqt = (S + BQ - 1) / BQ, nkt = (S + BKV - 1) / BKV;
-  const int smem_dq = 2 * G::ROW_BYTES + G::COL_BYTES;
+  const int smem_dq = 2 * G::ROW_BYTES + G::TR_BYTES;
   hipLaunchKernelGGL((attn_bwd_dq_kernel<HD>), dim3(B * H * nqt), dim3(256), smem_dq, st, (const bf16*)qkv.data_ptr(),
-                     (const bf16*)dout.data_ptr(), lse.data_ptr<float>(), Dv.data_ptr<float>(),
-                     (bf16*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
-  const int smem_kv = 2 * G::ROW_BYTES + 2 * G::COL_BYTES + 2 * 64 * 4;
+                     (const bf16*)o.data_ptr(), (const bf16*)dout.data_ptr(), lse.data_ptr<float>(),
+                     Dv.data_ptr<float>(), (bf16*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
+  const int smem_kv = 2 * G::ROW_BYTES + 2 * G::TR_BYTES + 2 * 64 * 4;
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD>), dim3(B * H * nkt), dim3(256), smem_kv, st,
                      (const bf16*)qkv.data_ptr(), (const bf16*)dout.data_ptr(), lse.data_ptr<float>(),
                      Dv.data_ptr<float>(), (bf16*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
@@ -498,13 +514,15 @@ std::vector<at::Tensor> mift_attn_fwd(const at::Tensor& qkv, int64_t B, int64_t 
     TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == B, "attn: kv_len int32 [B]");
     kvl = kv_len->data_ptr<int>();
   }
+  if (B * S == 0) return {o, lse};
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  const uint32_t thr = mift_thr16(p);
   const float inv_keep = p > 0 ? mift_inv_keep(p) : 1.f;
   switch (HD) {
-    case 64: fwd_launch<64>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr_of(p), inv_keep, st); break;
-    case 80: fwd_launch<80>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr_of(p), inv_keep, st); break;
-    case 128: fwd_launch<128>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr_of(p), inv_keep, st); break;
-    case 32: fwd_launch<32>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr_of(p), inv_keep, st); break;
+    case 64: fwd_launch<64>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
+    case 80: fwd_launch<80>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
+    case 128: fwd_launch<128>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
+    case 32: fwd_launch<32>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
     default: TORCH_CHECK(false, "attn: unsupported head dim ", HD);
   }
   return {o, lse};
@@ -516,14 +534,16 @@ at::Tensor mift_attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at
   TORCH_CHECK(dout.is_contiguous() && o.is_contiguous(), "attn_bwd: contiguous");
   auto dqkv = at::empty_like(qkv);
   auto Dv = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+  if (B * S == 0) return dqkv;
   const int* kvl = kv_len ? kv_len->data_ptr<int>() : nullptr;
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  const uint32_t thr = mift_thr16(p);
   const float inv_keep = p > 0 ? mift_inv_keep(p) : 1.f;
   switch (HD) {
-    case 64: bwd_launch<64>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr_of(p), inv_keep, st); break;
-    case 80: bwd_launch<80>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr_of(p), inv_keep, st); break;
-    case 128: bwd_launch<128>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr_of(p), inv_keep, st); break;
-    case 32: bwd_launch<32>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr_of(p), inv_keep, st); break;
+    case 64: bwd_launch<64>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
+    case 80: bwd_launch<80>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
+    case 128: bwd_launch<128>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
+    case 32: bwd_launch<32>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
     default: TORCH_CHECK(false, "attn_bwd: unsupported head dim ", HD);
   }
   return dqkv;
