@@ -9,7 +9,7 @@ rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
 agg = collections.defaultdict(lambda: [0, 0.0])
 for r in rows:
     name = r["Kernel_Name"]
-    short = name.split("(")[0]
+    short = name.replace("(anonymous namespace)::", "").split("(")[0]
     if "Cijk" in short:
         short = "hipBLASLt:" + short[:50]
     grid = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))

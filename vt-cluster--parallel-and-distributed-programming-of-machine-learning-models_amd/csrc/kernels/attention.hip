@@ -215,14 +215,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     float psum = 0.f;
     bf16x8 pf[2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      bool kp[4] = {true, true, true, true};
+      if (thr != 0) mift_keep4(seed, ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4, thr, kp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float p = (mnew == -INFINITY) ? 0.f : exp2f(st[t][r] - mnew);
         psum += p;
-        if (thr != 0) p = drop_keep(seed, thr, bh, S, myq, k0 + t * 16 + g * 4 + r) ? p * inv_keep : 0.f;
+        if (thr != 0) p = kp[r] ? p * inv_keep : 0.f;
         pf[t >> 1][(t & 1) * 4 + r] = (bf16)p;
       }
+    }
     l = l * alpha + psum;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -332,12 +335,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         sa = mfma_bf16(ld_frag(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], sa);
         pa = mfma_bf16(ld_frag(Vs + (t * 16 + qc) * G::RS + (4 * s + g) * 16), df[s], pa);
       }
+      bool kp[4] = {true, true, true, true};
+      if (thr != 0) mift_keep4(seed, ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4, thr, kp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + t * 16 + g * 4 + r;
         const float p = (key > myq || key >= klen) ? 0.f : exp2f(sa[r] * c2 - lse2);
         float dp = pa[r];
-        if (thr != 0) dp = drop_keep(seed, thr, bh, S, myq, key) ? dp * inv_keep : 0.f;
+        if (thr != 0) dp = kp[r] ? dp * inv_keep : 0.f;
         dsf[t >> 1][(t & 1) * 4 + r] = (bf16)(p * (dp - Dq));
       }
     }
@@ -435,7 +440,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
         sa = mfma_bf16(ld_frag(Qs + (t * 16 + kc) * G::RS + (4 * s + g) * 16), kf[s], sa);
         pa = mfma_bf16(ld_frag(dOs + (t * 16 + kc) * G::RS + (4 * s + g) * 16), vf[s], pa);
       }
-      // acc layout: row = query t*16 + g*4 + r, col = key kc
+      // acc layout: row = query t*16 + g*4 + r, col = key kc.  Dropout bits:
+      // keys (kc, kc^1) share one hash pair per query, so the even-key lane
+      // hashes queries r=0,1 and the odd-key lane r=2,3, then they swap.
+      uint32_t hb[4] = {0, 0, 0, 0};
+      if (thr != 0) {
+        const int odd = kc & 1;
+        const int qa = min(qb + t * 16 + g * 4 + 2 * odd, S - 1);
+        const uint64_t p0 = (((uint64_t)bh * S + qa) * S + mykey) >> 1;
+        const uint64_t p1 = (((uint64_t)bh * S + min(qa + 1, S - 1)) * S + mykey) >> 1;
+        const uint32_t h0 = mift_hash_pair(seed, p0), h1 = mift_hash_pair(seed, p1);
+        const uint32_t o0 = __shfl_xor(h0, 1, 64), o1 = __shfl_xor(h1, 1, 64);
+        hb[0] = odd ? o0 : h0;
+        hb[1] = odd ? o1 : h1;
+        hb[2] = odd ? h0 : o0;
+        hb[3] = odd ? h1 : o1;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = t * 16 + g * 4 + r;
@@ -444,7 +464,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
         const float p = valid ? exp2f(sa[r] * c2 - lse_s[ql]) : 0.f;
         float pd = p, dp = pa[r];
         if (thr != 0) {
-          const bool kp = valid && drop_keep(seed, thr, bh, S, q, mykey);
+          const uint32_t bits = (S & 1) ? mift_bits16(seed, ((uint64_t)bh * S + q) * S + mykey)
+                                        : ((hb[r] >> ((mykey & 1) << 4)) & 0xFFFFu);
+          const bool kp = valid && bits >= thr;
           pd = kp ? p * inv_keep : 0.f;
           dp = kp ? dp * inv_keep : 0.f;
         }

@@ -73,19 +73,52 @@ __global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X,
     for (int j = 0; j < 2; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
   const int rows[2] = {min(m0 + fr, M - 1), min(m0 + 16 + fr, M - 1)};
   const int nks = K / 32;
-#pragma unroll 2
-  for (int ks = wave; ks < nks; ks += 4) {
-    const int col = ks * 32 + g * 8;
-    frag_t<T> a[2], b[2];
+  // each wave owns a contiguous K range; UNR k-steps of loads are issued
+  // back to back before their MFMAs (memory-level parallelism: this kernel is
+  // latency-bound, one 16-B load per lane per operand per k-step)
+  constexpr int UNR = 4;
+  const int per = (nks + 3) / 4;
+  const int kbeg = wave * per, kend = min(nks, kbeg + per);
+  for (int ks0 = kbeg; ks0 < kend; ks0 += UNR) {
+    short8 ra[UNR][2], rb[UNR][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      a[i] = masked_frag<T>(X + (int64_t)rows[i] * ldx + col, seed, (uint64_t)rows[i] * K + col, thr, inv_keep);
+    for (int u = 0; u < UNR; ++u) {
+      const int col = min(ks0 + u, nks - 1) * 32 + g * 8;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const frag_t<T>*>(W + (int64_t)(j * 16 + fr) * K + col);
+      for (int i = 0; i < 2; ++i) ra[u][i] = *reinterpret_cast<const short8*>(X + (int64_t)rows[i] * ldx + col);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j) rb[u][j] = *reinterpret_cast<const short8*>(W + (int64_t)(j * 16 + fr) * K + col);
+    }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<T>(a[i], b[j], acc[i][j]);
+    for (int u = 0; u < UNR; ++u) {
+      if (ks0 + u >= kend) break;
+      const int col = (ks0 + u) * 32 + g * 8;
+      frag_t<T> a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        short8 v = ra[u][i];
+        if (thr != 0) {
+          bool kp[8];
+          mift_keep8(seed, (uint64_t)rows[i] * K + col, thr, kp);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            short s = v[e];
+            T t;
+            __builtin_memcpy(&t, &s, 2);
+            t = kp[e] ? (T)((float)t * inv_keep) : (T)0.f;
+            __builtin_memcpy(&s, &t, 2);
+            v[e] = s;
+          }
+        }
+        __builtin_memcpy(&a[i], &v, 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) __builtin_memcpy(&b[j], &rb[u][j], 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<T>(a[i], b[j], acc[i][j]);
+    }
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -115,8 +148,13 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X
                                                          float* __restrict__ out, int M, int P, int ldx,
                                                          int rows_per_block, uint64_t seed, uint32_t thr,
                                                          float inv_keep, int mode, int rank) {
-  __shared__ __attribute__((aligned(16))) char Xs[2][32 * XS];
-  __shared__ __attribute__((aligned(16))) char Ys[2][32 * YS];
+  // NB 32-row steps per group: the whole group's global loads are in flight
+  // together (one 16-B X load + half a Y load per thread per step), staged
+  // into NB LDS buffers, then consumed; the next group's loads are issued
+  // before this group's transpose reads + MFMAs.
+  constexpr int NB = 4;
+  __shared__ __attribute__((aligned(16))) char Xs[NB][32 * XS];
+  __shared__ __attribute__((aligned(16))) char Ys[NB][32 * YS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int ntp = P / 64;
@@ -126,38 +164,49 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X
   const int mend = min(mbeg + rows_per_block, M);
   float4_ acc[2] = {float4_{0.f, 0.f, 0.f, 0.f}, float4_{0.f, 0.f, 0.f, 0.f}};
 
-  // staging assignment: X: thread -> (row = tid/8, chunk = tid%8); Y: threads 0..127 -> (row = tid/4, chunk = tid%4)
   const int xr = tid >> 3, xc = tid & 7;
   const int yr = (tid & 127) >> 2, yc = tid & 3;
-  short8 xv, yv;
-  auto gload = [&](int m) {
-    const int gm = min(m + xr, M - 1);
-    const bool valid = (m + xr) < mend;
-    xv = *reinterpret_cast<const short8*>(X + (int64_t)gm * ldx + p0 + xc * 8);
-    if (thr != 0 || !valid) {
-      bool kp[8];
-      if (thr != 0) mift_keep8(seed, (uint64_t)gm * P + p0 + xc * 8, thr, kp);
+  short8 xv[NB], yv[NB];
+  auto gload = [&](int m0g) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        short s = xv[e];
-        T t;
-        __builtin_memcpy(&t, &s, 2);
-        float f = (float)t;
-        f = !valid ? 0.f : (thr != 0 ? (kp[e] ? f * inv_keep : 0.f) : f);
-        t = (T)f;
-        __builtin_memcpy(&s, &t, 2);
-        xv[e] = s;
+    for (int s = 0; s < NB; ++s) {
+      const int m = m0g + 32 * s;
+      const int gm = min(m + xr, M - 1);
+      xv[s] = *reinterpret_cast<const short8*>(X + (int64_t)gm * ldx + p0 + xc * 8);
+      if (tid < 128) {
+        const int gy = min(m + yr, M - 1);
+        yv[s] = *reinterpret_cast<const short8*>(Y + (int64_t)gy * 32 + yc * 8);
       }
     }
-    if (tid < 128) {
-      const int gy = min(m + yr, M - 1);
-      yv = *reinterpret_cast<const short8*>(Y + (int64_t)gy * 32 + yc * 8);
-      if ((m + yr) >= mend) yv = short8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
   };
-  auto lstore = [&](int buf) {
-    *reinterpret_cast<short8*>(Xs[buf] + xr * XS + xc * 16) = xv;
-    if (tid < 128) *reinterpret_cast<short8*>(Ys[buf] + yr * YS + yc * 16) = yv;
+  auto lstore = [&](int m0g) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      const int m = m0g + 32 * s;
+      const bool valid = (m + xr) < mend;
+      short8 v = xv[s];
+      if (thr != 0 || !valid) {
+        bool kp[8];
+        if (thr != 0) mift_keep8(seed, (uint64_t)min(m + xr, M - 1) * P + p0 + xc * 8, thr, kp);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          short sh = v[e];
+          T t;
+          __builtin_memcpy(&t, &sh, 2);
+          float f = (float)t;
+          f = !valid ? 0.f : (thr != 0 ? (kp[e] ? f * inv_keep : 0.f) : f);
+          t = (T)f;
+          __builtin_memcpy(&sh, &t, 2);
+          v[e] = sh;
+        }
+      }
+      *reinterpret_cast<short8*>(Xs[s] + xr * XS + xc * 16) = v;
+      if (tid < 128) {
+        short8 w = yv[s];
+        if ((m + yr) >= mend) w = short8{0, 0, 0, 0, 0, 0, 0, 0};
+        *reinterpret_cast<short8*>(Ys[s] + yr * YS + yc * 16) = w;
+      }
+    }
   };
 
   // transpose-read addresses (permuted rows: first read rows 4g+q', second 16+4g+q')
@@ -167,34 +216,32 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X
   const int yoff0 = rowA * YS + (0 * 16 + p4 * 4) * 2;
   const int yoff1 = rowA * YS + (1 * 16 + p4 * 4) * 2;
 
-  int buf = 0;
-  if (mbeg < mend) {
-    gload(mbeg);
-    lstore(0);
-  }
-  __syncthreads();
-  for (int m = mbeg; m < mend; m += 32) {
-    const bool more = m + 32 < mend;
-    if (more) gload(m + 32);
-    const char* xb = Xs[buf];
-    const char* yb = Ys[buf];
-    v4s a0 = tr_read<T>(xb, xoff), a1 = tr_read<T>(xb, xoff + 16 * XS);
-    v4s b00 = tr_read<T>(yb, yoff0), b01 = tr_read<T>(yb, yoff0 + 16 * YS);
-    v4s b10 = tr_read<T>(yb, yoff1), b11 = tr_read<T>(yb, yoff1 + 16 * YS);
-    frag_t<T> af, bf0, bf1;
-    {
-      short8 t = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      __builtin_memcpy(&af, &t, 16);
-      short8 u = {b00[0], b00[1], b00[2], b00[3], b01[0], b01[1], b01[2], b01[3]};
-      __builtin_memcpy(&bf0, &u, 16);
-      short8 w = {b10[0], b10[1], b10[2], b10[3], b11[0], b11[1], b11[2], b11[3]};
-      __builtin_memcpy(&bf1, &w, 16);
-    }
-    acc[0] = mfma16<T>(af, bf0, acc[0]);
-    acc[1] = mfma16<T>(af, bf1, acc[1]);
-    if (more) lstore(buf ^ 1);
+  if (mbeg < mend) gload(mbeg);
+  for (int mg = mbeg; mg < mend; mg += 32 * NB) {
     __syncthreads();
-    buf ^= 1;
+    lstore(mg);
+    __syncthreads();
+    if (mg + 32 * NB < mend) gload(mg + 32 * NB);
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      if (mg + 32 * s >= mend) break;
+      const char* xb = Xs[s];
+      const char* yb = Ys[s];
+      v4s a0 = tr_read<T>(xb, xoff), a1 = tr_read<T>(xb, xoff + 16 * XS);
+      v4s b00 = tr_read<T>(yb, yoff0), b01 = tr_read<T>(yb, yoff0 + 16 * YS);
+      v4s b10 = tr_read<T>(yb, yoff1), b11 = tr_read<T>(yb, yoff1 + 16 * YS);
+      frag_t<T> af, bf0, bf1;
+      {
+        short8 t = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        __builtin_memcpy(&af, &t, 16);
+        short8 u = {b00[0], b00[1], b00[2], b00[3], b01[0], b01[1], b01[2], b01[3]};
+        __builtin_memcpy(&bf0, &u, 16);
+        short8 w = {b10[0], b10[1], b10[2], b10[3], b11[0], b11[1], b11[2], b11[3]};
+        __builtin_memcpy(&bf1, &w, 16);
+      }
+      acc[0] = mfma16<T>(af, bf0, acc[0]);
+      acc[1] = mfma16<T>(af, bf1, acc[1]);
+    }
   }
   // acc[c][r] = out[p = p0 + wave*16 + g*4 + r][q = c*16 + li]
   // mode 0: dense [P,32]; mode 1: dB layout [P, rank]; mode 2: dA layout [rank, P]
@@ -249,8 +296,8 @@ void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, 
   }
   if (M == 0) return;
   const int ntp = P / 64;
-  int splits = std::max(1, std::min((512 + ntp - 1) / ntp, (M + 31) / 32));
-  int rows = ((M + splits - 1) / splits + 31) / 32 * 32;
+  int splits = std::max(1, std::min((512 + ntp - 1) / ntp, (M + 127) / 128));
+  int rows = ((M + splits - 1) / splits + 127) / 128 * 128;
   splits = (M + rows - 1) / rows;
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const uint32_t thr = mift_thr16(p);

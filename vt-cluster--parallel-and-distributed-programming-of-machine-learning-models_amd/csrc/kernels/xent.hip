@@ -98,6 +98,83 @@ __global__ __launch_bounds__(256) void xent_kernel(T* __restrict__ logits, const
   }
 }
 
+// Single-pass variant: the row lives in registers (NV 16-B vectors per
+// thread, 512 threads -> rows up to NV*4096 wide), so HBM traffic is one read
+// + one write of the logits (the 2-pass kernel above reads twice).
+template <typename T, int NV>
+__global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                       float* __restrict__ loss, float* __restrict__ lse_out, int V,
+                                                       int ldV, int64_t ignore_index, int write_grad) {
+  __shared__ float red[8];
+  __shared__ float lab_logit;
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  T* x = logits + (int64_t)row * ldV;
+  short8 v[NV];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 512 + tid) * 8;
+    if (c < ldV) {
+      v[k] = *reinterpret_cast<const short8*>(x + c);
+      float f[8];
+      load8<T>(reinterpret_cast<const T*>(&v[k]), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c + e < V) m = fmaxf(m, f[e]);
+    }
+  }
+  const int64_t lab = labels[row];
+  const bool valid = lab != ignore_index && lab >= 0 && lab < V;
+  if (tid == 0) lab_logit = valid ? (float)x[lab] : 0.f;
+  m = wave_max(m);
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  float M = red[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) M = fmaxf(M, red[i]);
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 512 + tid) * 8;
+    if (c < ldV) {
+      float f[8];
+      load8<T>(reinterpret_cast<const T*>(&v[k]), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c + e < V) s += __expf(f[e] - M);
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  float S = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) S += red[i];
+  const float lse = M + __logf(S);
+  if (tid == 0) {
+    loss[row] = valid ? (lse - lab_logit) : 0.f;
+    if (lse_out) lse_out[row] = lse;
+  }
+  if (!write_grad) return;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 512 + tid) * 8;
+    if (c < ldV) {
+      float f[8];
+      load8<T>(reinterpret_cast<const T*>(&v[k]), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int cc = c + e;
+        float p = (valid && cc < V) ? __expf(f[e] - lse) : 0.f;
+        if (valid && cc == lab) p -= 1.f;
+        f[e] = p;
+      }
+      store8<T>(x + c, f);
+    }
+  }
+}
+
 }  // namespace
 
 // logits [M, ldV] (modified in place into dlogits when write_grad) -> (loss[M], lse[M])
@@ -112,6 +189,20 @@ std::vector<at::Tensor> mift_xent_fwd_bwd(at::Tensor& logits, const at::Tensor& 
   if (M == 0) return {loss, lse};
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   auto lab = labels.contiguous();
+  const int nv = (ldV + 4095) / 4096;
+  if (logits.scalar_type() == at::kBFloat16 && nv <= 16) {
+#define XR(N) case N: xent_reg_kernel<bf16, N><<<M, 512, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), \
+                                                   loss.data_ptr<float>(), lse.data_ptr<float>(), (int)V, ldV, \
+                                                   ignore_index, write_grad ? 1 : 0); break;
+    switch (nv) { XR(1) XR(2) XR(4) XR(8) XR(12) XR(13) XR(16)
+      default:
+        if (nv <= 4) { xent_reg_kernel<bf16, 4><<<M, 512, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0); }
+        else if (nv <= 8) { xent_reg_kernel<bf16, 8><<<M, 512, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0); }
+        else { xent_reg_kernel<bf16, 16><<<M, 512, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0); }
+    }
+#undef XR
+    return {loss, lse};
+  }
   if (logits.scalar_type() == at::kBFloat16)
     xent_kernel<bf16><<<M, 256, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(),
                                          lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0);
