@@ -61,7 +61,7 @@ def bench_gemm(results):
         b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
         fl = 2.0 * M * N * K
         row = {"name": name, "M": M, "N": N, "K": K}
-        for tile in (0, 1, 2, 3):
+        for tile in (0, 1, 2, 3, 4):
             t = timeit(lambda: C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, tile, None, None, 0.0, 0))
             row[f"mift_t{tile}_ms"] = round(t, 4)
             row[f"mift_t{tile}_tflops"] = round(fl / t / 1e9, 1)

@@ -6,28 +6,32 @@
 // fragments want: a 16x16x32 A or B fragment is 8 consecutive K elements of
 // one row = one 16-byte ds_read_b128.  Frozen base weights are stored once
 // per orientation (W as [out,in] for forward, W^T as [in,out] for dgrad),
-// so forward and dgrad are both this kernel (see mift/ops/linear.py).
+// so forward and dgrad are both this kernel (see mift/models/layers.py).
 //
 // The optional A2/B2 pair is the LoRA "K-extension": with
 // T = s·dropout(X)·A^T (rank r<=32, zero padded to 32 columns) and
 // B2 = B (padded to [N,32]), one extra MFMA K-step adds the low-rank update
-// s·dropout(X)·A^T·B^T to the same accumulators as X·W^T — the adapter
-// costs one MFMA per output fragment instead of a second GEMM + add.
+// s·dropout(X)·A^T·B^T to the same accumulators as X·W^T.  In the dgrad the
+// extension is kept separate and added under the LoRA-input dropout mask.
 //
-// Tiling (gfx950): 256 threads = 4 waves (2x2), block tile BM x BN x 64,
-// each wave owns (BM/2) x (BN/2) as 16x16 MFMA tiles (mfma_f32_16x16x32).
-// Global->LDS staging by global_load_lds_dwordx4 (no VGPR round trip) into a
-// double-buffered, XOR-swizzled image (16-B chunk c of row r stored at chunk
-// c ^ (r & 7)) which makes every ds_read_b128 fragment read conflict-free
-// (checked with the lane-group model of the gfx950 LDS).  The swizzle is
-// applied on the per-lane global SOURCE address because the LDS-DMA
-// destination is lane-linear (guide rule 21).
+// Main loop (gfx950): NWM x NWN waves, block tile BM x BN x 64, each wave
+// owns (BM/NWM) x (BN/NWN) as 16x16 MFMA tiles (mfma_f32_16x16x32).
+// Global->LDS staging by global_load_lds_dwordx4 (no VGPR round trip) into
+// an NSTAGE-deep ring of XOR-swizzled images (16-B chunk c of row r stored at
+// chunk c ^ (r & 7): every ds_read_b128 fragment read is conflict-free;
+// swizzle applied on the per-lane global SOURCE address because the LDS-DMA
+// destination is lane-linear, guide rule 21).  NSTAGE-1 tiles are in flight:
+// each K step waits with a COUNTED s_waitcnt vmcnt (never 0 in steady state)
+// and a raw s_barrier, so the LDS-DMA of the next tiles overlaps the MFMAs
+// (guide §5 "Pipelining across barriers"; __syncthreads would drain it).
+// MFMA operands are swapped (A-slot = B tile) so accumulators hold four
+// consecutive output columns per lane (8-byte epilogue writes).
 //
-// Epilogue (two phases): accumulators (+bias) -> bf16 tile in LDS, then
-// every thread streams 8 consecutive columns (16-B loads/stores) applying
-// the elementwise tail: activation (gelu_new / relu / gelu_erf) with an
-// optional pre-activation output, activation-backward (dZ = dY ⊙ act'(z)),
-// dropout (counter hash, see common.h) and residual add.
+// Epilogue (two phases): accumulators (+bias, +masked LoRA ext) -> 16-bit
+// tile in LDS, then every thread streams 8 consecutive columns (16-B
+// loads/stores): pre-add, pre-activation output, activation (gelu_new / relu
+// / gelu_erf) or activation-backward (dZ = dY ⊙ act'(aux)), dropout (counter
+// hash, common.h) and residual add.
 //
 // Block order is XCD-aware (bijective remap, guide T1): blocks that share
 // an XCD (b, b+8, ...) walk the N tiles of the same A row panel.
@@ -91,21 +95,33 @@ MIFT_HD float apply_act(int act, float z, float aux) {
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;  // bytes per LDS row (128)
 
-template <typename T, int BM, int BN>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
-                                                         T* __restrict__ C, const T* __restrict__ A2,
-                                                         const T* __restrict__ B2, int M, int N, int K,
-                                                         int lda, int ldb, int ldc, EpiArgs ep) {
-  constexpr int WM = BM / 2, WN = BN / 2;      // wave tile
+// s_waitcnt vmcnt(n) with a compile-time n (0..63)
+template <int N>
+MIFT_HD void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE>
+__global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                                T* __restrict__ C, const T* __restrict__ A2,
+                                                                const T* __restrict__ B2, int M, int N, int K,
+                                                                int lda, int ldb, int ldc, EpiArgs ep) {
+  constexpr int NW = NWM * NWN;
+  constexpr int NT = NW * 64;
+  constexpr int WM = BM / NWM, WN = BN / NWN;  // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;    // MFMA tiles per wave
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;  // 1-KiB LDS-DMA pieces per stage
+  static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "stage pieces must split evenly over waves");
+  constexpr int PER_STAGE = (A_INSTR + B_INSTR) / NW;  // vmcnt units per stage per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWN, wn = wave % NWN;
 
   // ---- XCD-aware bijective block remap (T1) ----
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
@@ -119,29 +135,27 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
   const int tm = bid / ntn, tn = bid % ntn;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // ---- staging: each wave-instruction writes 1 KiB = 8 rows x 128 B ----
-  // lane -> (row-in-8 = lane>>3, physical chunk = lane&7); logical chunk =
-  // physical ^ (row & 7) -> per-lane source address.
+  // per-lane staging coordinates: lane -> (row-in-8 = lane>>3, phys chunk = lane&7)
+  const int srow = lane >> 3, spc = lane & 7;
   auto stage = [&](int buf, int k0) {
     char* base = smem + buf * STAGE_BYTES;
-    constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;  // per tile
 #pragma unroll
-    for (int i = wave; i < A_INSTR; i += 4) {
-      int r = i * 8 + (lane >> 3);
-      int pc = lane & 7;
-      int lc = pc ^ (r & 7);
-      int gr = min(m0 + r, M - 1);
-      const T* src = A + (size_t)gr * lda + k0 + lc * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + i * 1024), 16, 0, 0);
+    for (int ii = 0; ii < A_INSTR / NW; ++ii) {
+      const int i = wave + ii * NW;
+      const int r = i * 8 + srow;
+      const int lc = spc ^ (r & 7);
+      const int gr = min(m0 + r, M - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)gr * lda + k0 + lc * 8), (void*)(base + i * 1024),
+                                       16, 0, 0);
     }
 #pragma unroll
-    for (int i = wave; i < B_INSTR; i += 4) {
-      int r = i * 8 + (lane >> 3);
-      int pc = lane & 7;
-      int lc = pc ^ (r & 7);
-      int gr = min(n0 + r, N - 1);
-      const T* src = B + (size_t)gr * ldb + k0 + lc * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + A_BYTES + i * 1024), 16, 0, 0);
+    for (int ii = 0; ii < B_INSTR / NW; ++ii) {
+      const int i = wave + ii * NW;
+      const int r = i * 8 + srow;
+      const int lc = spc ^ (r & 7);
+      const int gr = min(n0 + r, N - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(B + (size_t)gr * ldb + k0 + lc * 8),
+                                       (void*)(base + A_BYTES + i * 1024), 16, 0, 0);
     }
   };
 
@@ -152,16 +166,26 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
     for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
-  stage(0, 0);
-  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0)
-  __syncthreads();
+  // prologue: NSTAGE-1 tiles in flight
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) stage(s, s * BK);
 
-  const int fr = lane & 15;      // fragment row
-  const int fq = lane >> 4;      // k sub-chunk (0..3)
-  int cur = 0;
+  const int fr = lane & 15;  // fragment row
+  const int fq = lane >> 4;  // k sub-chunk (0..3)
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
-    const char* As = smem + cur * STAGE_BYTES;
+    // tile kt landed <=> at most (#tiles issued after kt) * PER_STAGE pieces outstanding
+    if constexpr (NSTAGE >= 3) {
+      if (kt + 1 < nk) wait_vmcnt<PER_STAGE>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's pieces of kt landed; everyone done reading kt-1
+    asm volatile("" ::: "memory");  // no LDS access may move above the barrier
+    if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, (kt + NSTAGE - 1) * BK);
+    const char* As = smem + (kt % NSTAGE) * STAGE_BYTES;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -169,12 +193,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
       frag_t<T> af[TM], bfv[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        int r = wm * WM + i * 16 + fr;
+        const int r = wm * WM + i * 16 + fr;
         af[i] = *reinterpret_cast<const frag_t<T>*>(As + r * ROWB + ((lc ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        int r = wn * WN + j * 16 + fr;
+        const int r = wn * WN + j * 16 + fr;
         bfv[j] = *reinterpret_cast<const frag_t<T>*>(Bs + r * ROWB + ((lc ^ (r & 7)) << 4));
       }
 #pragma unroll
@@ -182,26 +206,20 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(bfv[j], af[i], acc[i][j]);
     }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    cur ^= 1;
   }
 
   // ---- LoRA K-extension: one extra K=32 step from global (A2[M,32], B2[N,32]) ----
-  // ext_thr == 0: accumulated into acc (forward: y += T·B^T).
-  // ext_thr != 0: kept separate and added in phase 1 under the dropout mask
-  //               (dgrad: dX += keep ⊙ (s·dT·A)/(1-p), mask of the LoRA input).
   frag_t<T> af2[TM], bf2[TN];
   const bool ext = A2 != nullptr;
   if (ext) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      int r = min(m0 + wm * WM + i * 16 + fr, M - 1);
+      const int r = min(m0 + wm * WM + i * 16 + fr, M - 1);
       af2[i] = *reinterpret_cast<const frag_t<T>*>(A2 + (size_t)r * 32 + fq * 8);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      int r = min(n0 + wn * WN + j * 16 + fr, N - 1);
+      const int r = min(n0 + wn * WN + j * 16 + fr, N - 1);
       bf2[j] = *reinterpret_cast<const frag_t<T>*>(B2 + (size_t)r * 32 + fq * 8);
     }
     if (ep.ext_thr == 0) {
@@ -213,12 +231,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
   }
   const bool ext_masked = ext && ep.ext_thr != 0;
 
-  // ---- epilogue phase 1: accumulators (*alpha, +bias, +masked LoRA ext) -> LDS tile ----
-  // MFMA operands are swapped (A-slot = B tile, B-slot = A tile), so the
-  // accumulator of tile (i,j) holds C[row = .. + fr][col = .. + 4*fq + e]:
-  // four CONSECUTIVE columns per lane -> one 8-byte ds_write per tile and two
-  // pair-hashes per four dropout decisions.
-  __syncthreads();  // staging buffers are reused for the C tile
+  // ---- epilogue phase 1: accumulators -> LDS tile (one 8-byte write per 16x16 tile) ----
+  __syncthreads();  // staging ring is reused for the C tile
   T* Cs = reinterpret_cast<T*>(smem);
   constexpr int CLD = BN + 8;
   const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
@@ -254,7 +268,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
 
   // ---- epilogue phase 2: 8 columns per thread, 16-B vector I/O, whole rows ----
   constexpr int VPR = BN / 8;
-  for (int v = tid; v < BM * VPR; v += 256) {
+  for (int v = tid; v < BM * VPR; v += NT) {
     const int row = v / VPR, c8 = (v % VPR) * 8;
     const int gr = m0 + row, gc = n0 + c8;
     if (gr >= M || gc >= N) continue;
@@ -300,41 +314,62 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const T* __restrict__ A
   }
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                  int K, const EpiArgs& ep, hipStream_t st) {
   constexpr int STAGE_BYTES = (BM + BN) * ROWB;
   constexpr int EPI_BYTES = BM * (BN + 8) * 2;
-  constexpr int SMEM = (2 * STAGE_BYTES > EPI_BYTES) ? 2 * STAGE_BYTES : EPI_BYTES;
+  constexpr int RING = NSTAGE * STAGE_BYTES;
+  constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
   const int nblk = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN>), dim3(nblk), dim3(256), SMEM, st, (const T*)a.data_ptr(),
-                     (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0),
-                     (int)b.stride(0), (int)c.stride(0), ep);
+  auto kern = gemm_nt_kernel<T, BM, BN, NWM, NWN, NSTAGE>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(NWM * NWN * 64), SMEM, st, (const T*)a.data_ptr(), (const T*)b.data_ptr(),
+                     (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), ep);
 }
 
+// Tile configurations (tile id -> geometry):
+//   1: 256x128, 8 waves (4x2), 3-stage ring (144 KiB, 1 block/CU)  — large N
+//   2: 128x64,  4 waves (2x2), 3-stage ring (72 KiB, 2 blocks/CU)  — N ~ 768
+//   3: 128x128, 4 waves (2x2), 2-stage ring (64 KiB, 2 blocks/CU)
+//   4: 64x64,   4 waves (2x2), 3-stage ring (48 KiB)               — tiny problems
 template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
-  // tile: 0 = auto
   if (tile == 0) {
+    // auto (measured on MI355X, tools/bench_kernels.py -> profiles/): the
+    // 256x128 3-stage ring wins on long-K, wide-N problems (OPT-2.7B qkv/fc1:
+    // +12-15%); the 128x128 tile wins everywhere else (distilgpt2 shapes:
+    // K = 768..3072) because its shorter prologue/epilogue dominates.
+    const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128);
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-    tile = (t128 >= 512) ? 1 : 2;
+    if (K >= 2048 && N >= 2048 && t256 >= 384) tile = 1;
+    else if (t128 >= 64) tile = 3;
+    else tile = 4;
   }
-  if (tile == 1) launch_gemm<T, 128, 128>(a, b, c, a2, b2, M, N, K, ep, st);
-  else if (tile == 2) launch_gemm<T, 128, 64>(a, b, c, a2, b2, M, N, K, ep, st);
-  else launch_gemm<T, 64, 64>(a, b, c, a2, b2, M, N, K, ep, st);
+  switch (tile) {
+    case 1: launch_gemm<T, 256, 128, 4, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 2: launch_gemm<T, 128, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 3: launch_gemm<T, 128, 128, 2, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    default: launch_gemm<T, 64, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
+  }
 }
 
 }  // namespace
 
 // out = epi(a @ b^T [+ a2 @ b2^T]).  a:[M,K], b:[N,K] (K-contiguous, K%64==0).
 std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
-                        const c10::optional<at::Tensor>& a2, const c10::optional<at::Tensor>& b2, int64_t act,
-                        const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& residual,
-                        double dropout_p, int64_t seed, bool want_preact, double alpha,
-                        const c10::optional<at::Tensor>& out, int64_t tile,
-                        const c10::optional<at::Tensor>& alpha_t, const c10::optional<at::Tensor>& pre_add,
-                        double ext_p, int64_t ext_seed) {
+                                     const c10::optional<at::Tensor>& a2, const c10::optional<at::Tensor>& b2,
+                                     int64_t act, const c10::optional<at::Tensor>& aux,
+                                     const c10::optional<at::Tensor>& residual, double dropout_p, int64_t seed,
+                                     bool want_preact, double alpha, const c10::optional<at::Tensor>& out,
+                                     int64_t tile, const c10::optional<at::Tensor>& alpha_t,
+                                     const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm_nt: GPU tensors required");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_nt: 2-D operands");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_nt: K must be contiguous");
@@ -397,6 +432,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                 "gemm_nt: pre_add layout must match out");
     ep.pre_add = pre_add->data_ptr();
   }
+  if (M == 0 || N == 0) return {c, pre};
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   if (a.scalar_type() == at::kBFloat16) {
     dispatch_tile<bf16>(a, b, c, a2 ? (const bf16*)a2->data_ptr() : nullptr, b2 ? (const bf16*)b2->data_ptr() : nullptr,
