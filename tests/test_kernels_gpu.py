@@ -155,12 +155,13 @@ def _attn_ref(qkv, B, S, H, hd, scale, p, seed, kv_len=None):
 @pytest.mark.parametrize("hd", [64, 80, 128])
 @pytest.mark.parametrize("S", [256, 200])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_flash_attention_fwd_bwd(hd, S, p):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_flash_attention_fwd_bwd(hd, S, p, dt):
     C = _C()
     torch.manual_seed(6)
     B, H = 2, 3
     scale = hd ** -0.5
-    qkv = (torch.randn(B * S, 3 * H * hd, device="cuda")).to(torch.bfloat16)
+    qkv = (torch.randn(B * S, 3 * H * hd, device="cuda")).to(dt)
     o, lse = C.attn_fwd(qkv, B, S, H, hd, scale, p, 321, None)
     x = qkv.float().requires_grad_(True)
     oref = _attn_ref(x, B, S, H, hd, scale, p, 321)
@@ -199,7 +200,7 @@ def test_lora_proj_and_wgrad(p):
     torch.testing.assert_close(out.float(), 2.0 * xd @ w.float().t(), atol=3e-2, rtol=3e-2)
     y = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
     acc = torch.zeros(K, 32, device="cuda")
-    C.lora_wgrad(x, y, acc, p, 55, 0, 32, 0)
+    C.lora_wgrad(x, y, acc, p, 55, 0, 32, 0, 0)
     exp = xd.t() @ y.float()
     err = (acc - exp).norm() / exp.norm()
     assert err < 1e-2, err

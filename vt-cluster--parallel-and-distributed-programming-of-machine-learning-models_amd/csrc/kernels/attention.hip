@@ -6,7 +6,7 @@
 // denominator of scale*QK^T) for the backward.  Head dims 32, 64 (GPT-2),
 // 80 (OPT-2.7B; QK^T K-steps zero-padded to 96) and 128 (OPT-6.7B).
 //
-// MFMA mapping (16x16x32 bf16, "swapped" products, guide §3):
+// MFMA mapping (16x16x32 bf16/f16, "swapped" products, guide §3):
 //   forward  S^T[key, q] = K · Q^T   A = K rows (LDS, ds_read_b128),
 //            B = Q rows (registers) -> each lane owns ONE query (lane & 15)
 //            and 4 keys per 16-key sub-tile, so the P tile already is the A
@@ -37,9 +37,18 @@ constexpr float LN2 = 0.6931471805599453f;
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 
-MIFT_HD float4_ mfma_bf16(bf16x8 a, bf16x8 b, float4_ c) {
+MIFT_HD float4_ mfma16(bf16x8 a, bf16x8 b, float4_ c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+MIFT_HD float4_ mfma16(fp16x8 a, fp16x8 b, float4_ c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// 8 x 16-bit MFMA operand vector of element type T (bf16 or fp16)
+template <typename T> struct V8;
+template <> struct V8<bf16> { using type = bf16x8; };
+template <> struct V8<fp16> { using type = fp16x8; };
+template <typename T> using vec8 = typename V8<T>::type;
 
 template <int HD>
 struct Geo {
@@ -55,24 +64,27 @@ struct Geo {
   static constexpr int NCH = (64 * CH + 255) / 256;  // chunks per thread per 64-row tile
 };
 
-MIFT_HD bf16x8 ld_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+template <typename T>
+MIFT_HD vec8<T> ld_frag(const char* p) { return *reinterpret_cast<const vec8<T>*>(p); }
 
-MIFT_HD bf16x8 zero_frag() {
-  bf16x8 z;
+template <typename T>
+MIFT_HD vec8<T> zero_frag() {
+  vec8<T> z;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+  for (int i = 0; i < 8; ++i) z[i] = (T)0.f;
   return z;
 }
 
 // B fragment from a row-major [key][hd] image by two transpose reads:
 // lane (li, g) gets X[kbase + 4g + 0..3][col0 + li] and X[kbase + 16 + 4g + 0..3][col0 + li]
-MIFT_HD bf16x8 tr_frag(const char* img, int stride, int kbase, int col0, int lane) {
+template <typename T>
+MIFT_HD vec8<T> tr_frag(const char* img, int stride, int kbase, int col0, int lane) {
   const int g = lane >> 4, li = lane & 15;
   const int off = (kbase + 4 * g + (li >> 2)) * stride + (col0 + (li & 3) * 4) * 2;
   v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + off));
   v4s b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + off + 16 * stride));
   short8 t = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  bf16x8 f;
+  vec8<T> f;
   __builtin_memcpy(&f, &t, 16);
   return f;
 }
@@ -81,7 +93,8 @@ MIFT_HD bf16x8 tr_frag(const char* img, int stride, int kbase, int col0, int lan
 template <int HD>
 struct TileRegs {
   short8 v[Geo<HD>::NCH];
-  MIFT_HD void load(const bf16* src, int64_t ld, int row0, int nrows, int tid) {
+  template <typename T>
+  MIFT_HD void load(const T* src, int64_t ld, int row0, int nrows, int tid) {
     using G = Geo<HD>;
 #pragma unroll
     for (int k = 0; k < G::NCH; ++k) {
@@ -118,14 +131,14 @@ MIFT_HD void zero_row_pad(char* dst, int tid) {
 }
 
 // fragments for 16 rows straight from global: frag[s] = X[row][32s + 8(lane>>4) ..]
-template <int HD>
-MIFT_HD void load_reg_frags(bf16x8* f, const bf16* src, int64_t ld, int row, int nrows, int lane) {
+template <typename T, int HD>
+MIFT_HD void load_reg_frags(vec8<T>* f, const T* src, int64_t ld, int row, int nrows, int lane) {
   using G = Geo<HD>;
   const int gr = min(row, nrows - 1);
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
     const int col = 32 * s + 8 * (lane >> 4);
-    f[s] = col < HD ? *reinterpret_cast<const bf16x8*>(src + (int64_t)gr * ld + col) : zero_frag();
+    f[s] = col < HD ? *reinterpret_cast<const vec8<T>*>(src + (int64_t)gr * ld + col) : zero_frag<T>();
   }
 }
 
@@ -134,8 +147,8 @@ MIFT_HD bool drop_keep(uint64_t seed, uint32_t thr, int64_t bh, int S, int q, in
 }
 
 // ============================== forward ====================================
-template <int HD>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ kv_len,
                                                        int B, int S, int H, float scale, uint64_t seed,
                                                        uint32_t thr, float inv_keep) {
@@ -151,16 +164,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
-  const bf16* Qg = qkv + (int64_t)b * S * ld + h * HD;
-  const bf16* Kg = Qg + D;
-  const bf16* Vg = Qg + 2 * D;
+  const T* Qg = qkv + (int64_t)b * S * ld + h * HD;
+  const T* Kg = Qg + D;
+  const T* Vg = Qg + 2 * D;
   const int klen = kv_len ? kv_len[b] : S;
   const int q0 = qt * BQ + wave * 16;
   const int myq = q0 + qc;
   const float c2 = scale * LOG2E;
 
-  bf16x8 qf[G::NKS];
-  load_reg_frags<HD>(qf, Qg, ld, myq, S, lane);
+  vec8<T> qf[G::NKS];
+  load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
   zero_row_pad<HD>(Ks, tid);
 
   float m = -INFINITY, l = 0.f;
@@ -191,7 +204,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
       st[t] = float4_{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < G::NKS; ++s)
-        st[t] = mfma_bf16(ld_frag(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], st[t]);
+        st[t] = mfma16(ld_frag<T>(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], st[t]);
     }
     const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
     float tmax = -INFINITY;
@@ -213,7 +226,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - mnew);
     m = mnew;
     float psum = 0.f;
-    bf16x8 pf[2];
+    vec8<T> pf[2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       bool kp[4] = {true, true, true, true};
@@ -223,7 +236,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
         float p = (mnew == -INFINITY) ? 0.f : exp2f(st[t][r] - mnew);
         psum += p;
         if (thr != 0) p = kp[r] ? p * inv_keep : 0.f;
-        pf[t >> 1][(t & 1) * 4 + r] = (bf16)p;
+        pf[t >> 1][(t & 1) * 4 + r] = (T)p;
       }
     }
     l = l * alpha + psum;
@@ -236,29 +249,29 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) o[i] = mfma_bf16(pf[s2], tr_frag(Vs, G::TRS, 32 * s2, i * 16, lane), o[i]);
+      for (int s2 = 0; s2 < 2; ++s2) o[i] = mfma16(pf[s2], tr_frag<T>(Vs, G::TRS, 32 * s2, i * 16, lane), o[i]);
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   const float inv_l = l > 0.f ? 1.f / l : 0.f;
   if (g == 0 && myq < S) lse[(int64_t)bh * S + myq] = (l > 0.f) ? (m + log2f(l)) * LN2 : -INFINITY;
-  bf16* Og = out + (int64_t)b * S * D + h * HD;
+  T* Og = out + (int64_t)b * S * D + h * HD;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float il = __shfl(inv_l, g * 4 + r, 64);
     const int q = q0 + g * 4 + r;
     if (q < S) {
 #pragma unroll
-      for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (bf16)(o[i][r] * il);
+      for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (T)(o[i][r] * il);
     }
   }
 }
 
 // ============================ backward: dQ (+D) =============================
-template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o,
-                                                          const bf16* __restrict__ dout, const float* __restrict__ lse,
-                                                          float* __restrict__ Dv, bf16* __restrict__ dqkv,
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
+                                                          const T* __restrict__ dout, const float* __restrict__ lse,
+                                                          float* __restrict__ Dv, T* __restrict__ dqkv,
                                                           const int* __restrict__ kv_len, int B, int S, int H,
                                                           float scale, uint64_t seed, uint32_t thr, float inv_keep) {
   using G = Geo<HD>;
@@ -274,24 +287,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
-  const bf16* Qg = qkv + (int64_t)b * S * ld + h * HD;
-  const bf16* Kg = Qg + D;
-  const bf16* Vg = Qg + 2 * D;
-  const bf16* dOg = dout + (int64_t)b * S * D + h * HD;
-  const bf16* Og = o + (int64_t)b * S * D + h * HD;
+  const T* Qg = qkv + (int64_t)b * S * ld + h * HD;
+  const T* Kg = Qg + D;
+  const T* Vg = Qg + 2 * D;
+  const T* dOg = dout + (int64_t)b * S * D + h * HD;
+  const T* Og = o + (int64_t)b * S * D + h * HD;
   const int klen = kv_len ? kv_len[b] : S;
   const int q0 = qt * BQ + wave * 16;
   const int myq = q0 + qc;
   const float c2 = scale * LOG2E;
 
-  bf16x8 qf[G::NKS], df[G::NKS];
-  load_reg_frags<HD>(qf, Qg, ld, myq, S, lane);
-  load_reg_frags<HD>(df, dOg, D, myq, S, lane);
+  vec8<T> qf[G::NKS], df[G::NKS];
+  load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
+  load_reg_frags<T, HD>(df, dOg, D, myq, S, lane);
   // D = rowsum(dO ∘ O) for this lane's query (fused attn_bwd_pre)
   float Dq = 0.f;
   {
-    bf16x8 of[G::NKS];
-    load_reg_frags<HD>(of, Og, D, myq, S, lane);
+    vec8<T> of[G::NKS];
+    load_reg_frags<T, HD>(of, Og, D, myq, S, lane);
 #pragma unroll
     for (int s = 0; s < G::NKS; ++s)
 #pragma unroll
@@ -326,14 +339,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
       kr.load(Kg, ld, k0 + BKV, S, tid);
       vr.load(Vg, ld, k0 + BKV, S, tid);
     }
-    bf16x8 dsf[2];
+    vec8<T> dsf[2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       float4_ sa = float4_{0.f, 0.f, 0.f, 0.f}, pa = float4_{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < G::NKS; ++s) {
-        sa = mfma_bf16(ld_frag(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], sa);
-        pa = mfma_bf16(ld_frag(Vs + (t * 16 + qc) * G::RS + (4 * s + g) * 16), df[s], pa);
+        sa = mfma16(ld_frag<T>(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], sa);
+        pa = mfma16(ld_frag<T>(Vs + (t * 16 + qc) * G::RS + (4 * s + g) * 16), df[s], pa);
       }
       bool kp[4] = {true, true, true, true};
       if (thr != 0) mift_keep4(seed, ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4, thr, kp);
@@ -343,30 +356,30 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         const float p = (key > myq || key >= klen) ? 0.f : exp2f(sa[r] * c2 - lse2);
         float dp = pa[r];
         if (thr != 0) dp = kp[r] ? dp * inv_keep : 0.f;
-        dsf[t >> 1][(t & 1) * 4 + r] = (bf16)(p * (dp - Dq));
+        dsf[t >> 1][(t & 1) * 4 + r] = (T)(p * (dp - Dq));
       }
     }
 #pragma unroll
     for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) dq[i] = mfma_bf16(dsf[s2], tr_frag(Kt, G::TRS, 32 * s2, i * 16, lane), dq[i]);
+      for (int s2 = 0; s2 < 2; ++s2) dq[i] = mfma16(dsf[s2], tr_frag<T>(Kt, G::TRS, 32 * s2, i * 16, lane), dq[i]);
   }
-  bf16* dQg = dqkv + (int64_t)b * S * ld + h * HD;
+  T* dQg = dqkv + (int64_t)b * S * ld + h * HD;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int q = q0 + g * 4 + r;
     if (q < S) {
 #pragma unroll
-      for (int i = 0; i < G::NOT; ++i) dQg[(int64_t)q * ld + i * 16 + qc] = (bf16)(dq[i][r] * scale);
+      for (int i = 0; i < G::NOT; ++i) dQg[(int64_t)q * ld + i * 16 + qc] = (T)(dq[i][r] * scale);
     }
   }
 }
 
 // ========================== backward: dK, dV ===============================
-template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ Dv,
-                                                            bf16* __restrict__ dqkv, const int* __restrict__ kv_len,
+                                                            T* __restrict__ dqkv, const int* __restrict__ kv_len,
                                                             int B, int S, int H, float scale, uint64_t seed,
                                                             uint32_t thr, float inv_keep) {
   using G = Geo<HD>;
@@ -385,18 +398,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
-  const bf16* Qg = qkv + (int64_t)b * S * ld + h * HD;
-  const bf16* Kg = Qg + D;
-  const bf16* Vg = Qg + 2 * D;
-  const bf16* dOg = dout + (int64_t)b * S * D + h * HD;
+  const T* Qg = qkv + (int64_t)b * S * ld + h * HD;
+  const T* Kg = Qg + D;
+  const T* Vg = Qg + 2 * D;
+  const T* dOg = dout + (int64_t)b * S * D + h * HD;
   const int klen = kv_len ? kv_len[b] : S;
   const int k0 = kt * BKV + wave * 16;
   const int mykey = k0 + kc;
   const float c2 = scale * LOG2E;
 
-  bf16x8 kf[G::NKS], vf[G::NKS];
-  load_reg_frags<HD>(kf, Kg, ld, mykey, S, lane);
-  load_reg_frags<HD>(vf, Vg, ld, mykey, S, lane);
+  vec8<T> kf[G::NKS], vf[G::NKS];
+  load_reg_frags<T, HD>(kf, Kg, ld, mykey, S, lane);
+  load_reg_frags<T, HD>(vf, Vg, ld, mykey, S, lane);
   zero_row_pad<HD>(Qs, tid);
   zero_row_pad<HD>(dOs, tid);
 
@@ -431,14 +444,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
       qr.load(Qg, ld, qb + BQ, S, tid);
       dr.load(dOg, D, qb + BQ, S, tid);
     }
-    bf16x8 pf[2], dsf[2];
+    vec8<T> pf[2], dsf[2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       float4_ sa = float4_{0.f, 0.f, 0.f, 0.f}, pa = float4_{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < G::NKS; ++s) {
-        sa = mfma_bf16(ld_frag(Qs + (t * 16 + kc) * G::RS + (4 * s + g) * 16), kf[s], sa);
-        pa = mfma_bf16(ld_frag(dOs + (t * 16 + kc) * G::RS + (4 * s + g) * 16), vf[s], pa);
+        sa = mfma16(ld_frag<T>(Qs + (t * 16 + kc) * G::RS + (4 * s + g) * 16), kf[s], sa);
+        pa = mfma16(ld_frag<T>(dOs + (t * 16 + kc) * G::RS + (4 * s + g) * 16), vf[s], pa);
       }
       // acc layout: row = query t*16 + g*4 + r, col = key kc.  Dropout bits:
       // keys (kc, kc^1) share one hash pair per query, so the even-key lane
@@ -470,64 +483,65 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
           pd = kp ? p * inv_keep : 0.f;
           dp = kp ? dp * inv_keep : 0.f;
         }
-        pf[t >> 1][(t & 1) * 4 + r] = (bf16)pd;
-        dsf[t >> 1][(t & 1) * 4 + r] = (bf16)(p * (dp - D_s[ql]));
+        pf[t >> 1][(t & 1) * 4 + r] = (T)pd;
+        dsf[t >> 1][(t & 1) * 4 + r] = (T)(p * (dp - D_s[ql]));
       }
     }
 #pragma unroll
     for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        dv[i] = mfma_bf16(pf[s2], tr_frag(dOt, G::TRS, 32 * s2, i * 16, lane), dv[i]);
-        dk[i] = mfma_bf16(dsf[s2], tr_frag(Qt, G::TRS, 32 * s2, i * 16, lane), dk[i]);
+        dv[i] = mfma16(pf[s2], tr_frag<T>(dOt, G::TRS, 32 * s2, i * 16, lane), dv[i]);
+        dk[i] = mfma16(dsf[s2], tr_frag<T>(Qt, G::TRS, 32 * s2, i * 16, lane), dk[i]);
       }
   }
-  bf16* dKg = dqkv + (int64_t)b * S * ld + D + h * HD;
-  bf16* dVg = dKg + D;
+  T* dKg = dqkv + (int64_t)b * S * ld + D + h * HD;
+  T* dVg = dKg + D;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int key = k0 + g * 4 + r;
     if (key < S) {
 #pragma unroll
       for (int i = 0; i < G::NOT; ++i) {
-        dKg[(int64_t)key * ld + i * 16 + kc] = (bf16)(dk[i][r] * scale);
-        dVg[(int64_t)key * ld + i * 16 + kc] = (bf16)dv[i][r];
+        dKg[(int64_t)key * ld + i * 16 + kc] = (T)(dk[i][r] * scale);
+        dVg[(int64_t)key * ld + i * 16 + kc] = (T)dv[i][r];
       }
     }
   }
 }
 
-template <int HD>
+template <typename T, int HD>
 void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int* kvl, int B, int S, int H, float scale,
                 uint64_t seed, uint32_t thr, float inv_keep, hipStream_t st) {
   using G = Geo<HD>;
   const int nqt = (S + BQ - 1) / BQ;
   const int smem = G::ROW_BYTES + G::TR_BYTES;
-  hipLaunchKernelGGL((attn_fwd_kernel<HD>), dim3(B * H * nqt), dim3(256), smem, st, (const bf16*)qkv.data_ptr(),
-                     (bf16*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, thr, inv_keep);
+  hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
+                     (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, thr, inv_keep);
 }
 
-template <int HD>
+template <typename T, int HD>
 void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
                 at::Tensor& Dv, at::Tensor& dqkv, const int* kvl, int B, int S, int H, float scale, uint64_t seed,
                 uint32_t thr, float inv_keep, hipStream_t st) {
   using G = Geo<HD>;
   const int nqt = (S + BQ - 1) / BQ, nkt = (S + BKV - 1) / BKV;
   const int smem_dq = 2 * G::ROW_BYTES + G::TR_BYTES;
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD>), dim3(B * H * nqt), dim3(256), smem_dq, st, (const bf16*)qkv.data_ptr(),
-                     (const bf16*)o.data_ptr(), (const bf16*)dout.data_ptr(), lse.data_ptr<float>(),
-                     Dv.data_ptr<float>(), (bf16*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD>), dim3(B * H * nqt), dim3(256), smem_dq, st, (const T*)qkv.data_ptr(),
+                     (const T*)o.data_ptr(), (const T*)dout.data_ptr(), lse.data_ptr<float>(),
+                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
   const int smem_kv = 2 * G::ROW_BYTES + 2 * G::TR_BYTES + 2 * 64 * 4;
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD>), dim3(B * H * nkt), dim3(256), smem_kv, st,
-                     (const bf16*)qkv.data_ptr(), (const bf16*)dout.data_ptr(), lse.data_ptr<float>(),
-                     Dv.data_ptr<float>(), (bf16*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, HD>), dim3(B * H * nkt), dim3(256), smem_kv, st,
+                     (const T*)qkv.data_ptr(), (const T*)dout.data_ptr(), lse.data_ptr<float>(),
+                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
 }
 
 }  // namespace
 
 std::vector<at::Tensor> mift_attn_fwd(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, int64_t HD, double scale,
                                       double p, int64_t seed, const c10::optional<at::Tensor>& kv_len) {
-  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.scalar_type() == at::kBFloat16, "attn: bf16 contiguous qkv");
+  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && (qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf),
+              "attn: bf16/fp16 contiguous qkv");
   TORCH_CHECK(qkv.numel() == B * S * 3 * H * HD, "attn: qkv shape");
   auto o = at::empty({B * S, H * HD}, qkv.options());
   auto lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
@@ -540,12 +554,16 @@ std::vector<at::Tensor> mift_attn_fwd(const at::Tensor& qkv, int64_t B, int64_t 
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const uint32_t thr = mift_thr16(p);
   const float inv_keep = p > 0 ? mift_inv_keep(p) : 1.f;
+  const bool half = qkv.scalar_type() == at::kHalf;
+#define MIFT_FWD(D)                                                                                         \
+  case D:                                                                                                   \
+    if (half) fwd_launch<fp16, D>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); \
+    else fwd_launch<bf16, D>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st);      \
+    break;
   switch (HD) {
-    case 64: fwd_launch<64>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
-    case 80: fwd_launch<80>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
-    case 128: fwd_launch<128>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
-    case 32: fwd_launch<32>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
+    MIFT_FWD(64) MIFT_FWD(80) MIFT_FWD(128) MIFT_FWD(32)
     default: TORCH_CHECK(false, "attn: unsupported head dim ", HD);
+#undef MIFT_FWD
   }
   return {o, lse};
 }
@@ -561,12 +579,19 @@ at::Tensor mift_attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const uint32_t thr = mift_thr16(p);
   const float inv_keep = p > 0 ? mift_inv_keep(p) : 1.f;
+  TORCH_CHECK(dout.scalar_type() == qkv.scalar_type() && o.scalar_type() == qkv.scalar_type(), "attn_bwd: dtype");
+  const bool half = qkv.scalar_type() == at::kHalf;
+#define MIFT_BWD(D)                                                                                          \
+  case D:                                                                                                    \
+    if (half) bwd_launch<fp16, D>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, \
+                                  inv_keep, st);                                                             \
+    else bwd_launch<bf16, D>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr,      \
+                             inv_keep, st);                                                                  \
+    break;
   switch (HD) {
-    case 64: bwd_launch<64>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
-    case 80: bwd_launch<80>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
-    case 128: bwd_launch<128>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
-    case 32: bwd_launch<32>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); break;
+    MIFT_BWD(64) MIFT_BWD(80) MIFT_BWD(128) MIFT_BWD(32)
     default: TORCH_CHECK(false, "attn_bwd: unsupported head dim ", HD);
+#undef MIFT_BWD
   }
   return dqkv;
 }

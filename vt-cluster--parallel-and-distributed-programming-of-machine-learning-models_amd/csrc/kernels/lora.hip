@@ -147,7 +147,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X, const T* __restrict__ Y,
                                                          float* __restrict__ out, int M, int P, int ldx,
                                                          int rows_per_block, uint64_t seed, uint32_t thr,
-                                                         float inv_keep, int mode, int rank) {
+                                                         float inv_keep, int mode, int rank, int qoff) {
   // NB 32-row steps per group: the whole group's global loads are in flight
   // together (one 16-B X load + half a Y load per thread per step), staged
   // into NB LDS buffers, then consumed; the next group's loads are issued
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X
       const int64_t pp = p0 + wave * 16 + g * 4 + r;
       const int q = c * 16 + li;
       if (mode == 0) atomicAdd(out + pp * 32 + q, acc[c][r]);
-      else if (q < rank) atomicAdd(out + (mode == 1 ? pp * rank + q : (int64_t)q * P + pp), acc[c][r]);
+      else if (q >= qoff && q < qoff + rank) atomicAdd(out + (mode == 1 ? pp * rank + (q - qoff) : (int64_t)(q - qoff) * P + pp), acc[c][r]);
     }
 }
 
@@ -284,7 +284,7 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
 // out fp32, accumulated: mode 0 -> out[P,32]; mode 1/2 -> out is a flat arena
 // and the result lands at out[offset:] in dB [P,r] / dA [r,P] layout.
 void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, double p, int64_t seed, int64_t mode,
-                     int64_t rank, int64_t offset) {
+                     int64_t rank, int64_t offset, int64_t qoff) {
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && y.is_contiguous() && y.size(1) == 32, "lora_wgrad: shapes");
   const int M = x.size(0), P = x.size(1);
   TORCH_CHECK(y.size(0) == M && P % 64 == 0, "lora_wgrad: P % 64 == 0");
@@ -305,11 +305,11 @@ void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, 
   if (x.scalar_type() == at::kBFloat16)
     lora_wgrad_kernel<bf16><<<ntp * splits, 256, 0, st>>>((const bf16*)x.data_ptr(), (const bf16*)y.data_ptr(),
                                                           out.data_ptr<float>() + offset, M, P, (int)x.stride(0), rows,
-                                                          (uint64_t)seed, thr, ik, (int)mode, (int)rank);
+                                                          (uint64_t)seed, thr, ik, (int)mode, (int)rank, (int)qoff);
   else
     lora_wgrad_kernel<fp16><<<ntp * splits, 256, 0, st>>>((const fp16*)x.data_ptr(), (const fp16*)y.data_ptr(),
                                                           out.data_ptr<float>() + offset, M, P, (int)x.stride(0), rows,
-                                                          (uint64_t)seed, thr, ik, (int)mode, (int)rank);
+                                                          (uint64_t)seed, thr, ik, (int)mode, (int)rank, (int)qoff);
 }
 
 // ------------------------------------------------------------ pack_lora_all

@@ -23,7 +23,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
 // ---- LoRA side path (kernels/lora.hip)
 at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed);
 void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, double p, int64_t seed, int64_t mode,
-                     int64_t rank, int64_t offset);
+                     int64_t rank, int64_t offset, int64_t qoff);
 void mift_pack_lora_all(const at::Tensor& arena, const at::Tensor& table, const at::Tensor& scales, at::Tensor& out,
                         int64_t max_elems);
 

@@ -1,0 +1,73 @@
+"""Shared machinery of the causal-LM families (GPT-2, OPT).
+
+Every family exposes the same engine-facing surface so the DDP trainer,
+the pipeline engine and the generator treat them alike:
+
+  * ``forward(input_ids, attention_mask, labels, hidden_states, ...)`` ->
+    ``{"loss", "logits", "ntokens"}`` on the head stage, ``{"hidden_states"}``
+    on a stage without a head (``layer_range`` / ``has_embed`` / ``has_head``
+    build only one pipeline stage's weights: SURVEY §6 — the reference OOMs
+    because every rank materialises the whole fp32 model first);
+  * ``seed`` / ``micro_step``: counter-based dropout seeds, so a block
+    recomputed under activation checkpointing — or re-run by the pipeline
+    engine's backward — draws bit-identical masks;
+  * ``lm_weight_padded()``: the tied LM head as a [V_pad, d] operand
+    (V rounded up to 128 so the GEMM and the xent kernel see aligned rows).
+"""
+import torch
+import torch.nn as nn
+
+from ..ops.dispatch import use_kernels
+from .layers import seed_for
+
+
+class CausalLMBase(nn.Module):
+    def _init_runtime(self, vocab_padded):
+        self.vocab_padded = vocab_padded
+        self.seed = 0
+        self.micro_step = 0
+        self.fused = True  # use HIP kernels for GPU tensors
+        self.recompute = False
+        self._head_cache = None
+
+    # subclasses: tied_embedding() -> nn.Parameter [V, d]; blocks() -> list
+
+    def lm_weight_padded(self):
+        """Tied LM head as ([V_pad, d], [d, V_pad]) with zero rows beyond the vocab."""
+        w = self.tied_embedding()
+        key = (w.data_ptr(), w.dtype, w.device)
+        if self._head_cache is None or self._head_cache[0] != key:
+            wp = torch.zeros(self.vocab_padded, w.shape[1], dtype=w.dtype, device=w.device)
+            wp[: w.shape[0]].copy_(w.detach())
+            self._head_cache = (key, wp, None)
+        return self._head_cache[1], self._head_cache[2]
+
+    def next_micro_step(self):
+        self.micro_step += 1
+
+    def embed_seed(self):
+        return seed_for(self.seed, self.micro_step, 1)
+
+    def _use_fused(self, t):
+        return self.fused and use_kernels(t)
+
+    def num_layers(self):
+        return self.config.num_layers()
+
+    def stage_parameters(self):
+        """(name, tensor) of everything this stage materialised (for memory reports)."""
+        return list(self.named_parameters())
+
+
+def shift_labels(labels, ignore_index=-100):
+    """labels[:, 1:] with an ignore column appended -> aligned with every row."""
+    out = torch.full_like(labels, ignore_index)
+    out[:, :-1] = labels[:, 1:]
+    return out
+
+
+def ref_lm_loss(logits, labels, ignore_index=-100, reduction="mean"):
+    """HF shifted causal-LM CE (fp32 logits)."""
+    sl = logits[:, :-1].reshape(-1, logits.shape[-1])
+    tl = labels[:, 1:].reshape(-1)
+    return torch.nn.functional.cross_entropy(sl.float(), tl, ignore_index=ignore_index, reduction=reduction)

@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import reference as ref
-from ..ops.dispatch import use_kernels
+from .base import CausalLMBase, ref_lm_loss
 from .layers import Embedding, LayerNorm, Linear, init_normal_, padded_vocab, seed_for
 
 
@@ -52,6 +52,9 @@ class GPT2Config:
         if name in ("gpt2-tiny", "tiny-gpt2"):
             return GPT2Config(n_layer=2, n_embd=64, n_head=2, n_inner=256, vocab_size=1000, n_positions=128)
         raise ValueError(f"unknown GPT-2 preset {name}")
+
+    def num_layers(self):
+        return self.n_layer
 
     def to_hf_dict(self):
         d = asdict(self)
@@ -117,7 +120,7 @@ class GPT2Block(nn.Module):
         return h + y2
 
 
-class GPT2LMHeadModel(nn.Module):
+class GPT2LMHeadModel(CausalLMBase):
     """HF-compatible GPT-2 LM.  ``forward(input_ids, attention_mask, labels)``."""
 
     def __init__(self, cfg: GPT2Config, dtype=torch.float32, device=None, layer_range=None,
@@ -139,11 +142,7 @@ class GPT2LMHeadModel(nn.Module):
              for i in range(n)])
         if has_head:
             self.transformer.ln_f = LayerNorm(cfg.n_embd, cfg.layer_norm_epsilon, dtype=dtype, device=device)
-        self.seed = 0
-        self.micro_step = 0
-        self.fused = True  # use HIP kernels for GPU tensors
-        self.recompute = False
-        self._head_cache = None
+        self._init_runtime(self.vocab_padded)
 
     # ---- init / misc ----
     def init_weights(self, seed=0):
@@ -157,21 +156,8 @@ class GPT2LMHeadModel(nn.Module):
     def blocks(self):
         return [b for b in self.transformer.h if isinstance(b, GPT2Block)]
 
-    def lm_weight_padded(self):
-        """Tied LM head as [V_pad, d] (zero rows beyond vocab) for the HIP GEMM."""
-        w = self.transformer.wte.weight
-        key = (w.data_ptr(), w.dtype, w.device)
-        if self._head_cache is None or self._head_cache[0] != key:
-            wp = torch.zeros(self.vocab_padded, w.shape[1], dtype=w.dtype, device=w.device)
-            wp[: w.shape[0]].copy_(w.detach())
-            self._head_cache = (key, wp, wp.t().contiguous())
-        return self._head_cache[1], self._head_cache[2]
-
-    def next_micro_step(self):
-        self.micro_step += 1
-
-    def embed_seed(self):
-        return seed_for(self.seed, self.micro_step, 1)
+    def tied_embedding(self):
+        return self.transformer.wte.weight
 
     # ---- reference path pieces ----
     def embed_ref(self, input_ids, attention_mask=None):
@@ -187,13 +173,7 @@ class GPT2LMHeadModel(nn.Module):
         logits = h @ self.transformer.wte.weight.t()
         if labels is None:
             return None, logits
-        sl = logits[:, :-1].reshape(-1, logits.shape[-1])
-        tl = labels[:, 1:].reshape(-1)
-        loss = torch.nn.functional.cross_entropy(sl.float(), tl, ignore_index=-100, reduction=reduction)
-        return loss, logits
-
-    def _use_fused(self, t):
-        return self.fused and use_kernels(t)
+        return ref_lm_loss(logits, labels, -100, reduction), logits
 
     def forward(self, input_ids=None, attention_mask=None, labels=None, hidden_states=None, reduction="mean",
                 return_logits=True):

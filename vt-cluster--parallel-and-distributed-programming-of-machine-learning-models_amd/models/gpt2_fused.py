@@ -52,10 +52,10 @@ def fused_forward(model, input_ids, attention_mask, labels, hidden_states, reduc
             h = block_forward(blk, h, seeds, training)
     if not model.has_head:
         return {"hidden_states": h}
-    w_nk, w_kn = model.lm_weight_padded()
+    w_nk, _ = model.lm_weight_padded()
     if labels is not None:
         sl = shift_labels(labels)
-        loss_sum = F.lm_head_xent(h, model.transformer.ln_f, w_nk, w_kn, sl, cfg.vocab_size, -100,
+        loss_sum = F.lm_head_xent(h, model.transformer.ln_f, w_nk, sl, cfg.vocab_size, -100,
                                   need_grad=torch.is_grad_enabled())
         ntok = (sl != -100).sum()
         loss = loss_sum / ntok.clamp(min=1) if reduction == "mean" else loss_sum

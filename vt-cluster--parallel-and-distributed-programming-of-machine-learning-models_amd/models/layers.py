@@ -77,6 +77,15 @@ class Linear(nn.Module):
     def has_lora(self):
         return self.lora_r > 0
 
+    # ---- adapter interface of the fused Functions (mift.ops.fused) ----
+    def lora_params(self):
+        """Trainable adapter tensors, in the order lora_ops().backward() returns grads."""
+        return [self.lora_A.weight, self.lora_B.weight] if self.lora_r > 0 else []
+
+    def lora_ops(self, dtype):
+        from ..ops.fused import AdapterOps
+        return AdapterOps(self, dtype)
+
     # ---- reference (autograd) path ----
     def forward(self, x, lora_seed=0):
         if self.conv1d:
@@ -97,6 +106,69 @@ class Linear(nn.Module):
         if self.lora_r:
             s += f", lora_r={self.lora_r}, scale={self.lora_scaling}"
         return s
+
+
+class ConcatLinear:
+    """Several Linears that read the same input, run as ONE GEMM.
+
+    OPT keeps q/k/v as separate ``nn.Linear`` (HF / PEFT key names), but on
+    the HIP path one [3d, d] GEMM (+ one multi-adapter LoRA K-extension, see
+    ``mift.ops.fused.MultiAdapterOps``) writes the fused qkv row that the
+    flash-attention kernel reads in place.  Not an nn.Module: it owns no
+    parameters, only cached concatenated views of its members' frozen
+    weights (rebuilt when any member weight moves)."""
+
+    def __init__(self, lins):
+        self.lins = list(lins)
+        self.in_features = self.lins[0].in_features
+        self.out_features = sum(l.out_features for l in self.lins)
+        self._cache = None
+
+    def spans(self):
+        n0 = 0
+        for l in self.lins:
+            yield l, n0, n0 + l.out_features
+            n0 += l.out_features
+
+    def _get(self):
+        key = tuple((l.weight.data_ptr(), l.weight.dtype) for l in self.lins)
+        if self._cache is None or self._cache[0] != key:
+            w_nk = torch.cat([l.w_nk() for l in self.lins], 0).contiguous()
+            w_kn = torch.cat([l.w_kn() for l in self.lins], 1).contiguous()
+            if all(l.bias is None for l in self.lins):
+                b = None
+            else:
+                b = torch.cat([l.bias.detach() if l.bias is not None else
+                               torch.zeros(l.out_features, dtype=w_nk.dtype, device=w_nk.device)
+                               for l in self.lins])
+            self._cache = (key, w_nk, w_kn, b)
+        return self._cache
+
+    def w_nk(self):
+        return self._get()[1]
+
+    def w_kn(self):
+        return self._get()[2]
+
+    @property
+    def bias(self):
+        return self._get()[3]
+
+    def fusable(self):
+        """One shared K-extension fits every member adapter (ranks <= 32 // n)."""
+        ad = [l for l in self.lins if l.lora_r > 0]
+        if not ad:
+            return True
+        w = 32 // len(ad)
+        return (all(l.lora_r <= w for l in ad) and len({l.lora_dropout for l in ad}) == 1
+                and len({getattr(l, "_arena", None) is None for l in ad}) == 1)
+
+    def lora_params(self):
+        return [p for l in self.lins for p in l.lora_params()]
+
+    def lora_ops(self, dtype):
+        from ..ops.fused import MultiAdapterOps
+        return MultiAdapterOps(self, dtype)
 
 
 class LayerNorm(nn.Module):

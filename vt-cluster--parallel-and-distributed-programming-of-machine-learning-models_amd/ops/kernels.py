@@ -31,13 +31,13 @@ def lora_wgrad(x, y32, out=None, p=0.0, seed=0):
     import torch
     if out is None:
         out = torch.zeros(x.shape[1], 32, dtype=torch.float32, device=x.device)
-    C().lora_wgrad(x, y32, out, float(p), int(seed), 0, 32, 0)
+    C().lora_wgrad(x, y32, out, float(p), int(seed), 0, 32, 0, 0)
     return out
 
 
-def lora_wgrad_into(x, y32, arena_grad, mode, rank, offset, p=0.0, seed=0):
+def lora_wgrad_into(x, y32, arena_grad, mode, rank, offset, p=0.0, seed=0, qoff=0):
     """Accumulate dropout(x).T @ y32 into a flat fp32 arena: mode 1 -> [P, rank] (dB), 2 -> [rank, P] (dA)."""
-    C().lora_wgrad(x, y32, arena_grad, float(p), int(seed), int(mode), int(rank), int(offset))
+    C().lora_wgrad(x, y32, arena_grad, float(p), int(seed), int(mode), int(rank), int(offset), int(qoff))
 
 
 def layer_norm_fwd(x, w, b, eps):
