@@ -1,5 +1,6 @@
 #!/usr/bin/env python
-"""Flagship benchmark: distilgpt2 LoRA DDP fine-tuning throughput on MI355X.
+"""Flagship benchmark: distilgpt2 LoRA DDP fine-tuning throughput on MI355X
+(``--model facebook/opt-2.7b [--pp S]``: the OPT LoRA pipeline-parallel configs).
 
 Metric/config from BASELINE.json config #2: distilgpt2 LoRA (r=8, alpha=16,
 dropout 0.05, targets c_attn,c_proj), bf16, seq_len 256, per-rank effective
@@ -29,11 +30,15 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="distilgpt2")
-    ap.add_argument("--seq_len", type=int, default=256)
+    ap.add_argument("--seq_len", type=int, default=None, help="default 256 (GPT-2) / 512 (OPT, P2 sbatch)")
     ap.add_argument("--batch", type=int, default=1)
-    ap.add_argument("--accum", type=int, default=32)
+    ap.add_argument("--accum", type=int, default=None, help="default 32 (P1) / 96 (P2 sbatch)")
     ap.add_argument("--fold_accum", type=int, default=1)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--micro_batch", type=int, default=0, help="regroup batch*accum into micro-batches of this size")
+    ap.add_argument("--pp", type=int, default=1, help="pipeline stages (world = dp x pp)")
+    ap.add_argument("--partition", default="balanced", choices=["uniform", "balanced"])
+    ap.add_argument("--zero", type=int, default=0)
+    ap.add_argument("--precision", default=None, choices=["bf16", "fp16"], help="default bf16 (GPT-2) / fp16 (OPT)")
     ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
                     help="fused = mift HIP kernels; torch = eager PyTorch ops on the same model (comparison)")
     ap.add_argument("--profile_dir", default=None, help="torch.profiler chrome trace of 3 steps")
@@ -51,7 +56,11 @@ def main():
     from mift.parallel import dist as D
     from mift.train.trainer import TrainConfig, Trainer
 
-    ctx = D.init(verbose=False, sanity=True)
+    is_opt = "opt" in a.model.lower()
+    a.seq_len = a.seq_len or (512 if is_opt else 256)
+    a.accum = a.accum or (96 if is_opt else 32)
+    a.precision = a.precision or ("fp16" if is_opt else "bf16")
+    ctx = D.init(pp=a.pp, verbose=False, sanity=True)
     if a.gpus != ctx.world:
         if ctx.rank == 0:
             print(f"warning: --gpus {a.gpus} != WORLD_SIZE {ctx.world}; using WORLD_SIZE", file=sys.stderr)
@@ -61,19 +70,34 @@ def main():
         assert mift.kernels_available(), f"HIP extension not loaded: {mift._ext.error()!r}"
     dtype = torch.bfloat16 if a.precision == "bf16" else torch.float16
 
-    model = build_causal_lm(a.model, dtype=dtype, device=ctx.device, seed=0)
-    L.inject(model, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["c_attn", "c_proj"],
+    split = None
+    kw = {}
+    if ctx.pp > 1:
+        from mift.models.opt import OPTConfig
+        from mift.models.gpt2 import GPT2Config
+        from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
+        mcfg = OPTConfig.preset(a.model) if is_opt else GPT2Config.preset(a.model)
+        split = partition_layers(mcfg.num_layers(), ctx.pp, a.partition, head_cost_layers(mcfg))
+        kw = dict(layer_range=stage_layer_range(split, ctx.pp_rank), has_embed=ctx.is_first_stage,
+                  has_head=ctx.is_last_stage)
+    model = build_causal_lm(a.model, dtype=dtype, device=ctx.device, seed=0, **kw)
+    targets = ["q_proj", "k_proj", "v_proj", "out_proj", "fc1", "fc2"] if is_opt else ["c_attn", "c_proj"]
+    L.inject(model, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=targets,
                                  base_model_name_or_path=a.model))
     if a.impl == "torch":
         model.fused = False
     per_rank = a.batch * a.accum
-    mb, acc = (per_rank, 1) if a.fold_accum else (a.batch, a.accum)
+    if a.micro_batch and per_rank % a.micro_batch == 0:
+        mb, acc = a.micro_batch, per_rank // a.micro_batch
+    else:
+        mb, acc = (per_rank, 1) if (a.fold_accum and ctx.pp == 1) else (a.batch, a.accum)
     total_steps = a.warmup + a.steps
-    ds = synthetic_openwebtext(per_rank * n * total_steps, a.seq_len, model.config.vocab_size,
+    ds = synthetic_openwebtext(per_rank * ctx.dp * total_steps, a.seq_len, model.config.vocab_size,
                                model.config.pad_token_id, seed=1234, full_length=True)
     batcher = MicroBatcher(ds, mb, acc, rank=ctx.dp_rank, world=ctx.dp)
     tr = Trainer(model, batcher, TrainConfig(epochs=1, batch=mb, accum=acc, lr=5e-5, precision=a.precision,
-                                             logging_steps=0, save_steps=0, step_log="none"), ctx)
+                                             logging_steps=0, save_steps=0, step_log="none", zero_stage=a.zero),
+                 ctx)
     model.train()
     steps = list(batcher.epoch(0))
     assert len(steps) >= total_steps
@@ -100,7 +124,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = t.item()
     ms = dt / a.steps * 1000.0
-    tokens_per_step = per_rank * a.seq_len * n
+    tokens_per_step = per_rank * a.seq_len * ctx.dp
     value = tokens_per_step / (ms / 1000.0)
     stats = tr.opt.stats()
     if a.profile_dir and ctx.rank == 0:
@@ -113,9 +137,11 @@ def main():
         prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
         with open(os.path.join(a.profile_dir, "table.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
+    par = f"dp{ctx.dp}" + (f"xpp{ctx.pp}" if ctx.pp > 1 else "") + ("+zero1" if a.zero and ctx.dp > 1 else "")
     if ctx.rank == 0:
+        kind = "PP" if ctx.pp > 1 else "DDP"
         out = {
-            "metric": "distilgpt2 LoRA DDP fine-tune throughput (tokens/sec, whole job)",
+            "metric": f"{a.model.split('/')[-1]} LoRA {kind} fine-tune throughput (tokens/sec, whole job)",
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": n,
@@ -126,10 +152,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": a.precision,
-            "data": "synthetic (OpenWebText-shaped random tokens, full 256-token lines); random-init weights",
-            "config": {"model": a.model, "global_batch": per_rank * n, "seq_len": a.seq_len,
-                       "parallelism": f"dp{n}", "per_rank_batch": f"{a.batch}x{a.accum}",
-                       "lora": "r8/a16/p0.05 c_attn,c_proj", "impl": a.impl,
+            "data": f"synthetic (OpenWebText-shaped random tokens, full {a.seq_len}-token lines); random-init weights",
+            "config": {"model": a.model, "global_batch": per_rank * ctx.dp, "seq_len": a.seq_len,
+                       "parallelism": par, "per_rank_batch": f"{a.batch}x{a.accum}", "micro_batch": f"{mb}x{acc}",
+                       "split": split, "lora": "r8/a16/p0.05 " + ",".join(targets), "impl": a.impl,
                        "tokens_per_gpu_per_s": round(value / n, 1),
                        "final_grad_norm": round(stats["grad_norm"], 4)},
         }

@@ -1,0 +1,125 @@
+"""Multi-process (gloo, CPU) coverage of the parallel engines.
+
+Every configuration trains the same tiny OPT for 2 optimizer steps on the same
+data and must reproduce the single-process run: DDP (dp2), pipeline (pp2,
+with dropout ON — masks are counter-based so stages agree exactly), DP×PP
+(dp2×pp2) and ZeRO-1 (dp2).  Also checks the 1F1B op order and the stage
+partitioner (reference split rule `P2/finetune_lora_opt_pp.py:156-162`).
+"""
+import pytest
+import torch
+
+from mift.parallel.pipeline import partition_layers, schedule_1f1b
+from mift.utils import harness
+
+
+def _worker(rank, world, pp=1, zero=0, steps=2, mb=2, accum=4, dropout=0.0, partition="uniform",
+            ckpt_dir=None, resume=None):
+    from mift import lora as L
+    from mift.data import MicroBatcher, synthetic_openwebtext
+    from mift.models import build_causal_lm
+    from mift.models.opt import OPTConfig
+    from mift.parallel import dist as D
+    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
+    from mift.train.trainer import TrainConfig, Trainer
+
+    ctx = D.init(pp=pp, verbose=False, sanity=True)
+    cfg = OPTConfig.preset("opt-tiny")
+    split = partition_layers(cfg.num_hidden_layers, ctx.pp, partition, head_cost_layers(cfg))
+    lr_ = stage_layer_range(split, ctx.pp_rank)
+    model = build_causal_lm("opt-tiny", seed=3, layer_range=lr_, has_embed=ctx.is_first_stage,
+                            has_head=ctx.is_last_stage)
+    model.config.dropout = dropout
+    L.inject(model, L.LoraConfig(r=4, lora_alpha=8, lora_dropout=0.05 if dropout else 0.0,
+                                 target_modules=["q_proj", "k_proj", "v_proj", "out_proj", "fc1", "fc2"]), seed=3)
+    model.seed = 11
+    ds = synthetic_openwebtext(64, 16, cfg.vocab_size, cfg.pad_token_id, seed=5, full_length=False, mean_tokens=10)
+    batcher = MicroBatcher(ds, mb, accum, rank=ctx.dp_rank, world=ctx.dp)
+    tc = TrainConfig(epochs=1, batch=mb, accum=accum, lr=1e-2, max_steps=steps, precision="fp32", logging_steps=1,
+                     step_log="none", zero_stage=zero, save_steps=1 if ckpt_dir else 0, output_dir=ckpt_dir,
+                     resume=resume)
+    tr = Trainer(model, batcher, tc, ctx)
+    hist = tr.train()
+    state = tr.adapter_state()
+    D.destroy()
+    return {"loss": [h["loss"] for h in hist], "gn": [h["grad_norm"] for h in hist], "state": state,
+            "split": split}
+
+
+def _close_runs(a, b, tol=1e-4):
+    assert len(a["loss"]) == len(b["loss"]) == 2
+    for x, y in zip(a["loss"], b["loss"]):
+        assert abs(x - y) <= tol * max(1.0, abs(y)), (a["loss"], b["loss"])
+    for x, y in zip(a["gn"], b["gn"]):
+        assert abs(x - y) <= 1e-3 * max(1.0, abs(y)), (a["gn"], b["gn"])
+    assert a["state"].keys() == b["state"].keys() and len(a["state"]) == 4 * 6 * 2
+    for k in a["state"]:
+        torch.testing.assert_close(a["state"][k], b["state"][k], atol=2e-5, rtol=1e-4)
+
+
+@pytest.fixture(scope="module")
+def single():
+    return harness.run(_worker, 1, accum=8)[0]
+
+
+@pytest.fixture(scope="module")
+def single_drop():
+    return harness.run(_worker, 1, accum=4, dropout=0.1)[0]
+
+
+def test_ddp_matches_single(single):
+    r = harness.run(_worker, 2, accum=4)
+    _close_runs(r[0], single)
+    assert r[1]["state"] == {}
+
+
+def test_pipeline_matches_single_with_dropout(single_drop):
+    r = harness.run(_worker, 2, pp=2, accum=4, dropout=0.1)
+    _close_runs(r[0], single_drop)
+
+
+def test_pipeline_4_stages_balanced(single_drop):
+    r = harness.run(_worker, 4, pp=4, accum=4, dropout=0.1, partition="balanced")
+    assert r[0]["split"] == [1, 1, 1, 1]
+    _close_runs(r[0], single_drop)
+
+
+def test_dp_x_pp_matches_single(single):
+    r = harness.run(_worker, 4, pp=2, accum=4)
+    _close_runs(r[0], single)
+
+
+def test_zero1_matches_single(single):
+    r = harness.run(_worker, 2, zero=1, accum=4)
+    _close_runs(r[0], single)
+
+
+def test_pp_checkpoint_resume(tmp_path, single_drop):
+    """Stop after step 1 (checkpoint), resume in a fresh 2-stage job -> same result as uninterrupted."""
+    d = str(tmp_path / "ck")
+    harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, steps=1, ckpt_dir=d)
+    r = harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, steps=2, ckpt_dir=d, resume="auto")
+    for k in single_drop["state"]:
+        torch.testing.assert_close(r[0]["state"][k], single_drop["state"][k], atol=2e-5, rtol=1e-4)
+
+
+def test_1f1b_schedule_order():
+    S, M = 4, 6
+    for s in range(S):
+        ops = schedule_1f1b(S, s, M)
+        assert sorted(ops) == sorted([("F", i) for i in range(M)] + [("B", i) for i in range(M)])
+        live, peak = 0, 0
+        for kind, i in ops:
+            live += 1 if kind == "F" else -1
+            peak = max(peak, live)
+            if kind == "B":
+                assert ("F", i) in ops[:ops.index(("B", i))]
+        assert peak == min(S - s, M)
+
+
+def test_partition_rules():
+    assert partition_layers(32, 4, "uniform") == [8, 8, 8, 8]
+    assert partition_layers(32, 5, "uniform") == [7, 7, 6, 6, 6]      # reference N//S + (i < N%S)
+    b = partition_layers(32, 4, "balanced", head_layers=1.6)
+    assert sum(b) == 32 and b[-1] < 8 and max(b[:-1]) <= 9
+    assert sum(partition_layers(32, 8, "balanced", head_layers=1.6)) == 32

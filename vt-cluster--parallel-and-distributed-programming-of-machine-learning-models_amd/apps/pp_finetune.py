@@ -1,0 +1,224 @@
+"""OPT LoRA fine-tuning with pipeline parallelism (+ optional DP and ZeRO-1) —
+the reference's W2 workload.
+
+CLI-compatible with ``Cluster/Project 2 - Course Project/finetune_lora_opt_pp.py:24-36``
+(``--model_name --data_file --seq_len --epochs --batch --accum --lr --logdir
+--out_root --ds_cfg``, unknown args ignored like ``parse_known_args``) and the
+launch env (``RANK/WORLD_SIZE/LOCAL_RANK`` with SLURM fallbacks,
+``PIPELINE_PARALLEL_SIZE`` defaulting to the world size, `:38-54`).
+
+``--ds_cfg`` accepts the DeepSpeed JSON the reference ships
+(`deepspeed_pp_zero1_cpu_activ.json`): ``train_micro_batch_size_per_gpu``,
+``zero_optimization.stage``, ``fp16/bf16.enabled``, ``optimizer.params``
+(betas, eps, weight_decay) and ``gradient_clipping`` are honoured; as in the
+reference, ``--accum`` and ``--lr`` from the CLI win (``engine.set_lr`` /
+``set_gradient_accumulation_steps``, `:207-208`).  Keys that only make sense
+for DeepSpeed-on-CPU (``cpu_offload``, ``partition_activations``,
+``cpu_checkpointing``) are accepted and ignored: 288 GB of HBM per GPU holds
+every stage's weights and in-flight activations.
+
+Outputs: P2 loss lines ``[R{r}] ep=.. step=.. loss=.. (+..s)`` from the last
+stage every 10 steps (`:219-224`), ``{logdir}/timing_rank{r}.log`` phases, and
+on rank 0 ``{out_root}/opt27b_lora_pp_{unix}/`` with the FULL PEFT adapter
+(gathered from all stages — the reference would have saved only stage 0's
+view), the tokenizer, and ``meta.json`` ``{"split": [...], "stages": S}``.
+"""
+import argparse
+import json
+import os
+import time
+
+import torch
+
+from .. import lora as L
+from ..data import MicroBatcher, is_saved_dataset_dir, load_pretokenized, read_text_lines, synthetic_openwebtext, \
+    tokenize_lines
+from ..data.tokenizer import load_tokenizer
+from ..models import build_causal_lm
+from ..obs.timing import PhaseLogger, p2_loss_line
+from ..parallel import dist as D
+from ..parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
+from ..train.trainer import TrainConfig, Trainer
+
+
+def build_argparser():
+    ap = argparse.ArgumentParser(description="mift LoRA fine-tune of OPT with pipeline parallelism")
+    ap.add_argument("--model_name", default="facebook/opt-2.7b")
+    ap.add_argument("--data_file", required=True, help="plain-text file (one example per line) or saved dataset dir")
+    ap.add_argument("--seq_len", type=int, default=1024)
+    ap.add_argument("--epochs", type=float, default=1)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--accum", type=int, default=64)
+    ap.add_argument("--lr", type=float, default=5e-5)
+    ap.add_argument("--logdir", default="logs")
+    ap.add_argument("--out_root", default=os.path.expanduser("~/finetuned"))
+    ap.add_argument("--ds_cfg", default="deepspeed_pp_zero1_cpu.json")
+    # mift extensions
+    ap.add_argument("--pp", type=int, default=None, help="pipeline stages (default $PIPELINE_PARALLEL_SIZE or world)")
+    ap.add_argument("--partition", choices=["uniform", "balanced"], default="balanced")
+    ap.add_argument("--precision", choices=["fp16", "bf16", "fp32"], default=None)
+    ap.add_argument("--micro_batch", type=int, default=0,
+                    help="GPU micro-batch: regroups batch*accum sequences per step into micro-batches of this "
+                         "size (same token-normalised update, fewer pipeline bubbles); 0 = keep --batch")
+    ap.add_argument("--zero", type=int, default=None, help="ZeRO stage override (0/1)")
+    ap.add_argument("--synthetic", type=int, default=-1, help="N synthetic lines (-1: only if data file missing)")
+    ap.add_argument("--base_weights", default=None)
+    ap.add_argument("--tokenizer", default=None)
+    ap.add_argument("--lora_r", type=int, default=8)
+    ap.add_argument("--lora_alpha", type=int, default=16)
+    ap.add_argument("--lora_dropout", type=float, default=0.05)
+    ap.add_argument("--target_modules", default="q_proj,k_proj,v_proj,out_proj,fc1,fc2")
+    ap.add_argument("--max_steps", type=int, default=-1)
+    ap.add_argument("--log_every", type=int, default=10)
+    ap.add_argument("--gradient_checkpointing", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--save_steps", type=int, default=0)
+    ap.add_argument("--resume", default=None)
+    ap.add_argument("--no_save", action="store_true")
+    return ap
+
+
+def read_ds_config(path):
+    """DeepSpeed JSON -> dict of the knobs we honour (missing file -> reference inline defaults)."""
+    d = {}
+    if path and os.path.isfile(path):
+        with open(path) as f:
+            d = json.load(f)
+    opt = d.get("optimizer", {}).get("params", {})
+    return {
+        "micro_batch": d.get("train_micro_batch_size_per_gpu"),
+        "zero_stage": int(d.get("zero_optimization", {}).get("stage", 1)),
+        "fp16": bool(d.get("fp16", {}).get("enabled", False)),
+        "bf16": bool(d.get("bf16", {}).get("enabled", False)),
+        "betas": tuple(opt.get("betas", (0.9, 0.999))),
+        "eps": float(opt.get("eps", 1e-8)),
+        "weight_decay": float(opt.get("weight_decay", 0.0)),
+        "clip": float(d.get("gradient_clipping", 1.0)),
+        "found": bool(d),
+    }
+
+
+def main(argv=None):
+    args, _unknown = build_argparser().parse_known_args(argv)
+    world_env = int(os.environ.get("WORLD_SIZE", os.environ.get("SLURM_NTASKS", "1")))
+    stages = args.pp or int(os.environ.get("PIPELINE_PARALLEL_SIZE", str(world_env)))
+    assert 1 <= stages <= 32, "PIPELINE_PARALLEL_SIZE must be in [1,32]"
+    ctx = D.init(pp=stages)
+    rank = ctx.rank
+
+    def log(msg):
+        print(f"[R{rank}] {msg}", flush=True)
+
+    gpu = ctx.device.type == "cuda"
+    ds = read_ds_config(args.ds_cfg)
+    precision = args.precision or ("fp32" if not gpu else ("bf16" if ds["bf16"] else "fp16"))
+    if not gpu:
+        precision = "fp32"
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[precision]
+    zero = args.zero if args.zero is not None else ds["zero_stage"]
+    logs = PhaseLogger(args.logdir, rank)
+
+    # ---- data (every stage of a replica reads the same shard: DP rank, not global rank) ----
+    t0 = time.perf_counter()
+    use_synth = args.synthetic > 0 or (args.synthetic < 0 and not os.path.exists(args.data_file))
+    if use_synth:
+        log(f"Data file {args.data_file} not found: synthetic OpenWebText-shaped lines")
+    elif is_saved_dataset_dir(args.data_file):
+        log(f"Loading pre-tokenized dataset from disk: {args.data_file}")
+    else:
+        log(f"Loading RAW text file: {args.data_file}")
+    lines = None if (use_synth or is_saved_dataset_dir(args.data_file)) else read_text_lines(args.data_file)
+    logs.log("Dataset load", time.perf_counter() - t0, echo=False)
+
+    # ---- stage model: only this stage's layers are ever allocated ----
+    t0 = time.perf_counter()
+    from ..models.opt import OPTConfig
+    cfg = OPTConfig.preset(args.model_name)
+    N = cfg.num_hidden_layers
+    split = partition_layers(N, ctx.pp, args.partition, head_cost_layers(cfg))
+    lo, hi = stage_layer_range(split, ctx.pp_rank)
+    model = build_causal_lm(args.model_name, dtype=dtype, device=ctx.device, seed=args.seed,
+                            weights=args.base_weights, layer_range=(lo, hi), has_embed=ctx.is_first_stage,
+                            has_head=ctx.is_last_stage)
+    lcfg = L.LoraConfig(r=args.lora_r, lora_alpha=args.lora_alpha, lora_dropout=args.lora_dropout,
+                        target_modules=args.target_modules.split(","), base_model_name_or_path=args.model_name)
+    L.inject(model, lcfg, seed=args.seed)
+    model.seed = args.seed
+    log(f"Pipeline split={split} (total blocks={N}, stages={ctx.pp}) -> my layers [{lo},{hi})")
+    logs.log("Model build", time.perf_counter() - t0, echo=False)
+
+    # ---- tokenization ----
+    t0 = time.perf_counter()
+    tok = None
+    if use_synth:
+        n = args.synthetic if args.synthetic > 0 else 4096
+        data = synthetic_openwebtext(n, args.seq_len, cfg.vocab_size, cfg.pad_token_id, seed=1234)
+    elif lines is None:
+        data = load_pretokenized(args.data_file, args.seq_len, cfg.pad_token_id, cfg.vocab_size)
+        log("Detected tokenized dataset")
+    else:
+        tok = load_tokenizer(args.tokenizer or args.model_name, corpus_lines=lines, vocab_size=cfg.vocab_size)
+        log(f"Detected raw text; tokenizing (seq_len={args.seq_len})")
+        data = tokenize_lines(lines, tok, args.seq_len, cfg.pad_token_id, cfg.vocab_size)
+    logs.log("Tokenization", time.perf_counter() - t0, echo=False)
+
+    # ---- engine ----
+    t0 = time.perf_counter()
+    mb = ds["micro_batch"] or args.batch
+    per_step = mb * args.accum
+    if args.micro_batch and per_step % args.micro_batch == 0:
+        mb = args.micro_batch
+    accum = per_step // mb
+    batcher = MicroBatcher(data, mb, accum, rank=ctx.dp_rank, world=ctx.dp)
+    tcfg = TrainConfig(epochs=args.epochs, batch=mb, accum=accum, lr=args.lr, precision=precision,
+                       weight_decay=ds["weight_decay"], max_grad_norm=ds["clip"], logging_steps=args.log_every,
+                       step_log="none", max_steps=args.max_steps, seed=args.seed, zero_stage=zero,
+                       recompute=bool(args.gradient_checkpointing), save_steps=args.save_steps,
+                       output_dir=os.path.join(args.out_root, "checkpoints") if args.save_steps else None,
+                       resume=args.resume)
+    t_last = [time.perf_counter()]
+
+    def p2_log(trainer, rec):
+        if ctx.is_last_stage and ctx.dp_rank == 0:
+            now = time.perf_counter()
+            ep = int((trainer.global_step - 1) // max(1, trainer.steps_per_epoch))
+            print(p2_loss_line(rank, ep, trainer.global_step - 1, rec["loss"], now - t_last[0]), flush=True)
+            t_last[0] = now
+
+    trainer = Trainer(model, batcher, tcfg, ctx, callbacks=[p2_log])
+    log(f"engine initialized (stage {ctx.pp_rank}/{ctx.pp}, dp {ctx.dp_rank}/{ctx.dp}, mb={mb}x{accum}, "
+        f"{precision}, zero={zero})")
+    logs.log("Trainer setup", time.perf_counter() - t0, echo=False)
+
+    D.barrier()
+    t0 = time.perf_counter()
+    trainer.train()
+    if gpu:
+        torch.cuda.synchronize()
+    train_secs = time.perf_counter() - t0
+    logs.log("Training", train_secs)
+    D.barrier()
+
+    t0 = time.perf_counter()
+    state = trainer.adapter_state()
+    out = None
+    if rank == 0 and not args.no_save:
+        out = os.path.join(args.out_root, f"opt27b_lora_pp_{int(time.time())}")
+        L.save_adapter(out, state, lcfg)
+        if tok is not None:
+            tok.save_pretrained(out)
+        with open(os.path.join(out, "meta.json"), "w") as f:
+            json.dump({"split": split, "stages": ctx.pp}, f, indent=2)
+        log(f"Saved adapters+tokenizer to {out}")
+    logs.log("Model save", time.perf_counter() - t0, echo=False)
+    tokens = trainer.global_step * per_step * args.seq_len * ctx.dp
+    if rank == 0:
+        print(f"[R0] TRAIN_RUNTIME_SEC={train_secs:.3f} tokens_per_sec={tokens / max(train_secs, 1e-9):.1f} "
+              f"steps={trainer.global_step}", flush=True)
+    D.destroy()
+    return {"train_seconds": train_secs, "steps": trainer.global_step, "save_dir": out, "split": split,
+            "history": trainer.history}
+
+
+if __name__ == "__main__":
+    main()

@@ -62,8 +62,8 @@ def inject(model: nn.Module, cfg: LoraConfig, seed: int = 0, device=None) -> Lis
     """Attach LoRA matrices to every Linear whose name matches; freeze the base.
 
     Returns the adapted module names (in module order)."""
+    from ..models.layers import name_generator
     names = []
-    gen = torch.Generator().manual_seed(seed)
     for name, m in model.named_modules():
         if isinstance(m, Linear) and _matches(name, cfg.target_modules):
             dev = device or m.weight.device
@@ -72,7 +72,9 @@ def inject(model: nn.Module, cfg: LoraConfig, seed: int = 0, device=None) -> Lis
             # PEFT init: A ~ kaiming_uniform(a=sqrt(5)) => U(-1/sqrt(in), 1/sqrt(in)); B = 0
             bound = 1.0 / math.sqrt(m.in_features)
             with torch.no_grad():
-                a = torch.empty(cfg.r, m.in_features).uniform_(-bound, bound, generator=gen)
+                # per-module RNG stream: a pipeline stage draws what the full model would
+                a = torch.empty(cfg.r, m.in_features).uniform_(-bound, bound,
+                                                               generator=name_generator(seed, name + ".lora_A"))
                 m.lora_A.weight.copy_(a)
                 m.lora_B.weight.zero_()
             m.lora_r = cfg.r
@@ -95,7 +97,7 @@ def lora_parameters(model: nn.Module):
 class LoraArena:
     """Flat fp32 storage for all LoRA params + grads (see module doc)."""
 
-    def __init__(self, model: nn.Module, device=None, align: int = 64):
+    def __init__(self, model: nn.Module, device=None, align: int = 64, shards: int = 1):
         self.named = lora_parameters(model)
         if not self.named:
             raise ValueError("model has no LoRA parameters (call mift.lora.inject first)")
@@ -105,6 +107,8 @@ class LoraArena:
         for _, p in self.named:
             self.offsets.append(off)
             off += (p.numel() + align - 1) // align * align
+        q = align * shards  # ZeRO-1: equal, aligned shards of the flat buffers
+        off = (off + q - 1) // q * q
         self.numel = off
         self.n_real = sum(p.numel() for _, p in self.named)
         self.param = torch.zeros(off, dtype=torch.float32, device=device)

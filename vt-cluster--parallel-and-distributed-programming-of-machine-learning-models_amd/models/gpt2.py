@@ -146,11 +146,8 @@ class GPT2LMHeadModel(CausalLMBase):
 
     # ---- init / misc ----
     def init_weights(self, seed=0):
-        g = torch.random.fork_rng(devices=[])
-        with g:
-            torch.manual_seed(seed)
-            std = self.config.initializer_range
-            init_normal_(self, std, proj_std=std / (2 * self.config.n_layer) ** 0.5)
+        std = self.config.initializer_range
+        init_normal_(self, std, proj_std=std / (2 * self.config.n_layer) ** 0.5, seed=seed)
         return self
 
     def blocks(self):

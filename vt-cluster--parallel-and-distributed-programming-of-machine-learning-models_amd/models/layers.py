@@ -14,6 +14,7 @@ once and cached (HBM3E is 288 GB: the extra copy buys a single MFMA layout
 for every GEMM — see csrc/kernels/gemm.hip).
 """
 import math
+import zlib
 
 import torch
 import torch.nn as nn
@@ -198,18 +199,30 @@ def seed_for(base: int, step: int, site: int) -> int:
     return x & ((1 << 63) - 1)
 
 
-def init_normal_(module: nn.Module, std: float, proj_std: float = None, proj_names=("c_proj",)):
-    """HF-style init: N(0, std) weights, zero biases, unit LayerNorm."""
+def name_generator(seed: int, name: str, device=None) -> torch.Generator:
+    """RNG keyed by (seed, parameter name): a pipeline stage that builds only some
+    layers draws exactly the values the full model would (stage-local init)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "meta":
+        return None
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed_for(seed, 0, zlib.crc32(name.encode())))
+    return g
+
+
+def init_normal_(module: nn.Module, std: float, proj_std: float = None, proj_names=("c_proj",), seed: int = 0):
+    """HF-style init: N(0, std) weights, zero biases, unit LayerNorm (per-name RNG streams)."""
     for name, m in module.named_modules():
-        if isinstance(m, Linear):
-            s = proj_std if (proj_std is not None and any(name.endswith(p) for p in proj_names)) else std
+        if isinstance(m, (Linear, Embedding)):
+            s = std
+            if isinstance(m, Linear) and proj_std is not None and any(name.endswith(p) for p in proj_names):
+                s = proj_std
             with torch.no_grad():
-                m.weight.normal_(0.0, s)
-                if m.bias is not None:
+                g = name_generator(seed, name, m.weight.device)
+                if g is not None:
+                    m.weight.normal_(0.0, s, generator=g)
+                if isinstance(m, Linear) and m.bias is not None:
                     m.bias.zero_()
-        elif isinstance(m, Embedding):
-            with torch.no_grad():
-                m.weight.normal_(0.0, std)
         elif isinstance(m, LayerNorm):
             with torch.no_grad():
                 m.weight.fill_(1.0)

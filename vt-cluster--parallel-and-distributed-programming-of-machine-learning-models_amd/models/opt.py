@@ -204,9 +204,7 @@ class OPTForCausalLM(CausalLMBase):
         self._init_runtime(padded_vocab(cfg.vocab_size))
 
     def init_weights(self, seed=0):
-        with torch.random.fork_rng(devices=[]):
-            torch.manual_seed(seed)
-            init_normal_(self, self.config.init_std)
+        init_normal_(self, self.config.init_std, seed=seed)
         return self
 
     def tied_embedding(self):

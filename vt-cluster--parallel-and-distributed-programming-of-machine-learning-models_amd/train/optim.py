@@ -40,7 +40,10 @@ class FusedAdamW:
         self.state = torch.tensor([0.0, scale, 0.0, 1.0, 0.0, 0.0], dtype=torch.float32, device=dev)
         self.stats_buf = torch.zeros(2, dtype=torch.float32, device=dev)
         self.growth_interval = growth_interval
-        self.group = reduce_stats_group
+        # sum(g^2) / non-finite count are summed over every group holding a disjoint part
+        # of the parameters (pipeline stages, ZeRO-1 shards)
+        g = reduce_stats_group
+        self.groups = [x for x in (g if isinstance(g, (list, tuple)) else [g]) if x is not None]
         self.kernels = use_kernels(params)
 
     # ---- scaling ----
@@ -58,8 +61,9 @@ class FusedAdamW:
         else:
             self.stats_buf[0] = (self.g * self.g).sum()
             self.stats_buf[1] = (~torch.isfinite(self.g)).sum().float()
-        if self.group is not None and dist.is_initialized():
-            dist.all_reduce(self.stats_buf, group=self.group)
+        if dist.is_initialized():
+            for grp in self.groups:
+                dist.all_reduce(self.stats_buf, group=grp)
         if self.kernels:
             K.opt_finalize(self.stats_buf, self.state, float(self.max_grad_norm or 0.0), self.dynamic, 2.0, 0.5,
                            self.growth_interval)

@@ -56,6 +56,7 @@ class TrainConfig:
     bucket_mb: float = 25.0
     recompute: bool = False
     shuffle: bool = False
+    zero_stage: int = 0                # 1: shard AdamW state over the DP group (mift.parallel.zero)
 
 
 class Trainer:
@@ -65,16 +66,34 @@ class Trainer:
         self.device = ctx.device if ctx else torch.device("cpu")
         self.dp_group = ctx.dp_group if ctx else None
         self.dp = ctx.dp if ctx else 1
-        self.arena = LoraArena(model, device=self.device)
+        self.pp = ctx.pp if ctx else 1
+        self.zero = cfg.zero_stage >= 1 and self.dp > 1
+        self.arena = LoraArena(model, device=self.device, shards=self.dp if self.zero else 1)
         if self.device.type == "cuda" and getattr(model, "fused", False):
             from ..lora.pack import attach
             from ..ops.dispatch import use_kernels
             if use_kernels(self.arena.param):
                 attach(model, self.arena, next(p for n, p in model.named_parameters() if "lora_" not in n).dtype)
-        self.reducer = GradReducer(self.arena, group=self.dp_group, bucket_mb=cfg.bucket_mb, world=self.dp)
-        self.opt = FusedAdamW(self.arena.param, self.arena.grad, lr=cfg.lr, weight_decay=cfg.weight_decay,
-                              max_grad_norm=cfg.max_grad_norm,
-                              loss_scale="dynamic" if cfg.precision == "fp16" else "none")
+        okw = dict(lr=cfg.lr, weight_decay=cfg.weight_decay, max_grad_norm=cfg.max_grad_norm,
+                   loss_scale="dynamic" if cfg.precision == "fp16" else "none")
+        pp_group = ctx.pp_group if (ctx and self.pp > 1) else None
+        if self.zero:
+            from ..parallel.zero import Zero1AdamW
+            self.reducer = None
+            self.opt = Zero1AdamW(self.arena, self.dp_group, self.dp, ctx.dp_rank, stats_groups=[pp_group], **okw)
+        else:
+            # PP interleaves micro-batch backwards, so its DP all-reduce runs once after the schedule
+            self.reducer = GradReducer(self.arena, group=self.dp_group, bucket_mb=cfg.bucket_mb, world=self.dp,
+                                       overlap=self.pp == 1)
+            self.opt = FusedAdamW(self.arena.param, self.arena.grad, reduce_stats_group=pp_group, **okw)
+        self.engine = None
+        if self.pp > 1:
+            from ..parallel.pipeline import PipelineEngine
+            act_dtype = next(p for n, p in model.named_parameters() if "lora_" not in n).dtype
+            if self.device.type == "cpu" and cfg.precision == "bf16":
+                act_dtype = torch.float32
+            hidden = getattr(model.config, "hidden_size", None) or model.config.n_embd
+            self.engine = PipelineEngine(model, ctx, act_dtype, hidden)
         spe = batcher.steps_per_epoch()
         self.steps_per_epoch = spe
         total = int(math.ceil(spe * cfg.epochs))
@@ -122,13 +141,20 @@ class Trainer:
         lr = self.sched(self.global_step)
         self.opt.set_lr(lr)
         gscale = self.opt.loss_scale_t / ntok
+        if self.engine is not None:
+            dev_mbs = [self._to_dev(mb) for mb in mbs]
+            ms0 = model.micro_step
+            loss_acc = self.engine.train_batch(dev_mbs, gscale, ms0 + 1)
+            model.micro_step = ms0 + len(mbs)
+            maybe_inject(self.rank, self.global_step + 1, "micro")
+            return self._finish_step(loss_acc, ntok)
         loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
         autocast = (self.device.type == "cpu" and cfg.precision == "bf16")
         for i, mb in enumerate(mbs):
             mb = self._to_dev(mb)
             model.next_micro_step()
             last = i == len(mbs) - 1
-            ctxm = self.reducer.no_sync() if not last else _null()
+            ctxm = self.reducer.no_sync() if (not last and self.reducer is not None) else _null()
             with ctxm:
                 with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
                     out = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"],
@@ -137,12 +163,27 @@ class Trainer:
                 (loss_sum * gscale).backward()
             loss_acc += loss_sum.detach()
             maybe_inject(self.rank, self.global_step + 1, "micro")
+        return self._finish_step(loss_acc, ntok)
+
+    def _finish_step(self, loss_acc, ntok):
         self.arena.rebind_grads()
-        self.reducer.finish()
+        if self.zero:
+            self.opt.reduce_grads()
+        else:
+            self.reducer.finish()
         self.opt.step()
         self.arena.bump()
         self.global_step += 1
         return loss_acc, ntok
+
+    def _loss_for_log(self, loss_sum):
+        """Global summed token loss of the step on every rank (sum over DP replicas;
+        in PP only the last stage holds a loss, the others contribute 0)."""
+        if self.ctx is None or self.ctx.world == 1 or not dist.is_initialized():
+            return float(loss_sum)
+        t = loss_sum.detach().clone() if loss_sum is not None else torch.zeros((), device=self.device)
+        dist.all_reduce(t)
+        return float(t)
 
     # ------------------------------------------------------------------
     def train(self):
@@ -155,7 +196,6 @@ class Trainer:
         sync_dev = self.device.type == "cuda"
         epoch = start_step // max(1, self.steps_per_epoch)
         done = start_step >= self.total_steps
-        log_loss, log_tok = 0.0, 0
         while not done:
             skip = start_step - epoch * self.steps_per_epoch
             for mbs in self.batcher.epoch(epoch, start_step=max(0, skip)):
@@ -174,10 +214,9 @@ class Trainer:
                         sps = samples / max(dt, 1e-9)
                         seq = mbs[0]["input_ids"].shape[1]
                         print(lab_step_line(self.rank, self.global_step, dt * 1000, sps, sps * seq), flush=True)
-                log_loss += float(loss_sum) if (cfg.logging_steps and self.global_step % cfg.logging_steps == 0) else 0.0
                 if cfg.logging_steps and self.global_step % cfg.logging_steps == 0:
                     st = self.opt.stats()
-                    rec = {"loss": float(loss_sum) / max(1, ntok) * (self.dp if False else 1),
+                    rec = {"loss": self._loss_for_log(loss_sum) / max(1, ntok),
                            "grad_norm": st["grad_norm"], "learning_rate": self.sched(self.global_step),
                            "epoch": round(self.global_step / max(1, self.steps_per_epoch), 4)}
                     self.history.append(dict(rec, step=self.global_step))
@@ -202,23 +241,39 @@ class Trainer:
     def save_checkpoint(self):
         """``checkpoint-<step>/``: adapter + optimizer + rng + trainer_state (+rotation)."""
         out = os.path.join(self.cfg.output_dir, f"checkpoint-{self.global_step}")
+        state = self.adapter_state()
         if self.rank == 0:
             os.makedirs(out, exist_ok=True)
-            save_adapter(out, adapter_state_dict(self.model), self.model.lora_config)
-            torch.save(self.opt.state_dict(), os.path.join(out, "optimizer.pt"))
+            save_adapter(out, state, self.model.lora_config)
             with open(os.path.join(out, "trainer_state.json"), "w") as f:
                 json.dump({"global_step": self.global_step, "max_steps": self.total_steps,
                            "steps_per_epoch": self.steps_per_epoch, "log_history": self.history,
-                           "micro_step": self.model.micro_step, "seed": self.model.seed}, f, indent=2)
+                           "micro_step": self.model.micro_step, "seed": self.model.seed,
+                           "world": self.ctx.world if self.ctx else 1, "dp": self.dp, "pp": self.pp,
+                           "zero_stage": int(self.zero)}, f, indent=2)
         if dist.is_initialized():
             dist.barrier(group=self.ctx.ctrl_group if self.ctx else None)
+        # optimizer state is per rank in PP (stage-local adapters) and ZeRO-1 (shards)
+        torch.save(self.opt.state_dict(), os.path.join(out, self._opt_file()))
         torch.save({"cpu": torch.get_rng_state()}, os.path.join(out, f"rng_state_{self.rank}.pth"))
+        if dist.is_initialized():
+            dist.barrier(group=self.ctx.ctrl_group if self.ctx else None)
         if self.rank == 0 and self.cfg.save_total_limit:
             cks = sorted([d for d in os.listdir(self.cfg.output_dir) if d.startswith("checkpoint-")],
                          key=lambda d: int(d.split("-")[1]))
             for d in cks[:-self.cfg.save_total_limit]:
                 shutil.rmtree(os.path.join(self.cfg.output_dir, d), ignore_errors=True)
         return out
+
+    def _opt_file(self):
+        return "optimizer.pt" if (self.pp == 1 and not self.zero) else f"optimizer_rank{self.rank}.pt"
+
+    def adapter_state(self):
+        """Full PEFT adapter state (gathered over pipeline stages) on rank 0."""
+        if self.pp > 1:
+            from ..parallel.pipeline import gather_adapter_state
+            return gather_adapter_state(self.model, self.ctx)
+        return adapter_state_dict(self.model) if self.rank == 0 else {}
 
     def resume(self, spec):
         path = spec
@@ -231,7 +286,7 @@ class Trainer:
             path = os.path.join(self.cfg.output_dir, max(cks, key=lambda d: int(d.split("-")[1])))
         from ..lora import load_adapter
         load_adapter(self.model, path)
-        self.opt.load_state_dict(torch.load(os.path.join(path, "optimizer.pt"), weights_only=True))
+        self.opt.load_state_dict(torch.load(os.path.join(path, self._opt_file()), weights_only=True))
         with open(os.path.join(path, "trainer_state.json")) as f:
             st = json.load(f)
         self.global_step = st["global_step"]
