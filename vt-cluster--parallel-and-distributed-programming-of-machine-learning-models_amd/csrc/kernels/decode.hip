@@ -1,0 +1,140 @@
+// K12: single-token decode attention over a KV cache (greedy generation).
+//
+// Reference: HF ``generate(max_new_tokens=16)`` on distilgpt2 in the lab probe
+// (`run_labs45_tiny_final.sbatch:80-82`) — each decode step is a
+// forward over the KV cache.
+//
+// One 256-thread workgroup per (batch row, head).  The step's fused qkv row
+// [B, 3*H*HD] (straight from the qkv GEMM) supplies q and the NEW k/v, which
+// are (a) appended to the cache at position t and (b) used directly for key t
+// (never re-read from the cache inside this launch).  Cache layout
+// [B, H, Tmax, HD] keeps one head's keys contiguous, so the score pass is one
+// thread per key with 16-B row loads and the P·V pass maps threads to
+// (head-dim lane, key group) so each wave reads whole V rows coalesced.
+// Left padding: keys < start[b] are masked (HF left-padded batched generate).
+// Decode is HBM/latency bound (B·H·t·HD·2·2 bytes per layer): no MFMA.
+#include "common.h"
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+namespace {
+
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ qkv, T* __restrict__ kc,
+                                                          T* __restrict__ vc, T* __restrict__ out,
+                                                          const int* __restrict__ start, int H, int Tmax, int t,
+                                                          float scale) {
+  constexpr int G = 256 / HD;  // key groups in the P·V pass
+  extern __shared__ float sm[];
+  float* qs = sm;              // [HD]
+  float* red = qs + HD;        // [G*HD] (also used for the block reductions)
+  float* sc = red + G * HD;    // [t+1]
+  const int bh = blockIdx.x, b = bh / H, h = bh % H, tid = threadIdx.x;
+  const int64_t ld = 3LL * H * HD;
+  const T* qg = qkv + (int64_t)b * ld + h * HD;
+  const T* kg = qg + (int64_t)H * HD;
+  const T* vg = qg + 2LL * H * HD;
+  T* kcb = kc + (int64_t)bh * Tmax * HD;
+  T* vcb = vc + (int64_t)bh * Tmax * HD;
+  for (int i = tid; i < HD; i += 256) {
+    qs[i] = (float)qg[i] * scale;
+    kcb[(int64_t)t * HD + i] = kg[i];
+    vcb[(int64_t)t * HD + i] = vg[i];
+  }
+  __syncthreads();
+  const int s0 = start ? start[b] : 0;
+  float mx = -INFINITY;
+  for (int j = tid; j <= t; j += 256) {
+    float s = -INFINITY;
+    if (j >= s0) {
+      const T* kr = (j == t) ? kg : kcb + (int64_t)j * HD;
+      s = 0.f;
+#pragma unroll
+      for (int c = 0; c < HD; c += 8) {
+        float kv[8];
+        load8<T>(kr + c, kv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += qs[c + e] * kv[e];
+      }
+    }
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  const int lane = tid & 63, w = tid >> 6;
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  const float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int j = tid; j <= t; j += 256) {
+    const float p = sc[j] == -INFINITY ? 0.f : __expf(sc[j] - M);
+    sc[j] = p;
+    sum += p;
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[w] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[0] + red[1] + red[2] + red[3]);
+  __syncthreads();
+  const int d = tid % HD, g = tid / HD;
+  float acc = 0.f;
+  if (g < G) {
+    for (int j = s0 + g; j <= t; j += G) {
+      const T* vr = (j == t) ? vg : vcb + (int64_t)j * HD;
+      acc += sc[j] * (float)vr[d];
+    }
+    red[g * HD + d] = acc;
+  }
+  __syncthreads();
+  if (g == 0) {
+    float o = 0.f;
+#pragma unroll
+    for (int k = 0; k < G; ++k) o += red[k * HD + d];
+    out[(int64_t)b * H * HD + h * HD + d] = (T)(o * inv);
+  }
+}
+
+template <typename T, int HD>
+void launch(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, at::Tensor& out, const int* start, int B, int H,
+            int Tmax, int t, float scale, hipStream_t st) {
+  constexpr int G = 256 / HD;
+  const size_t smem = (size_t)(HD + G * HD + t + 1) * sizeof(float);
+  hipLaunchKernelGGL((decode_attn_kernel<T, HD>), dim3(B * H), dim3(256), smem, st, (const T*)qkv.data_ptr(),
+                     (T*)kc.data_ptr(), (T*)vc.data_ptr(), (T*)out.data_ptr(), start, H, Tmax, t, scale);
+}
+
+}  // namespace
+
+// qkv [B, 3*H*HD]; kc/vc [B, H, Tmax, HD] (row t written); start [B] int32 or None -> o [B, H*HD]
+at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
+                            const c10::optional<at::Tensor>& start) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 2, "decode_attn: qkv [B, 3*H*HD] contiguous");
+  TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.sizes() == vc.sizes(),
+              "decode_attn: caches [B,H,Tmax,HD]");
+  TORCH_CHECK(kc.scalar_type() == qkv.scalar_type() && vc.scalar_type() == qkv.scalar_type(), "decode_attn: dtype");
+  const int B = kc.size(0), H = kc.size(1), Tmax = kc.size(2), HD = kc.size(3);
+  TORCH_CHECK(qkv.size(0) == B && qkv.size(1) == 3LL * H * HD, "decode_attn: qkv/cache shape mismatch");
+  TORCH_CHECK(t >= 0 && t < Tmax, "decode_attn: position ", t, " outside cache of ", Tmax);
+  TORCH_CHECK(t < 16384, "decode_attn: context too long for the LDS score buffer");
+  const int* sp = nullptr;
+  if (start) {
+    TORCH_CHECK(start->scalar_type() == at::kInt && start->numel() == B && start->is_cuda(), "decode_attn: start");
+    sp = start->data_ptr<int>();
+  }
+  auto out = at::empty({B, H * HD}, qkv.options());
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  const bool half = qkv.scalar_type() == at::kHalf;
+  TORCH_CHECK(half || qkv.scalar_type() == at::kBFloat16, "decode_attn: bf16/fp16");
+#define MIFT_DEC(D)                                                                        \
+  case D:                                                                                  \
+    if (half) launch<fp16, D>(qkv, kc, vc, out, sp, B, H, Tmax, (int)t, (float)scale, st); \
+    else launch<bf16, D>(qkv, kc, vc, out, sp, B, H, Tmax, (int)t, (float)scale, st);      \
+    break;
+  switch (HD) {
+    MIFT_DEC(32) MIFT_DEC(64) MIFT_DEC(80) MIFT_DEC(128)
+    default: TORCH_CHECK(false, "decode_attn: unsupported head dim ", HD);
+  }
+#undef MIFT_DEC
+  return out;
+}

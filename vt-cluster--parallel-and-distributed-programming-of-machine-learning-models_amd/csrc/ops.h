@@ -54,7 +54,12 @@ at::Tensor mift_attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at
                          int64_t B, int64_t S, int64_t H, int64_t HD, double scale, double p, int64_t seed,
                          const c10::optional<at::Tensor>& kv_len);
 
+// ---- K12 decode attention over a KV cache (kernels/decode.hip)
+at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
+                            const c10::optional<at::Tensor>& start);
+
 #define MIFT_BIND_MORE(m) \
+  m.def("decode_attn", &mift_decode_attn, "single-token attention over a KV cache; appends k/v at t"); \
   m.def("lora_proj", &mift_lora_proj, "out[M,32] = alpha*drop(x)@w^T (tall-skinny MFMA)"); \
   m.def("lora_wgrad", &mift_lora_wgrad, "out[P,32] += drop(x)^T @ y (tr_b16 split-M MFMA); arena modes"); \
   m.def("pack_lora_all", &mift_pack_lora_all, "pack every adapter's 16-bit operands from the fp32 arena"); \

@@ -1,0 +1,167 @@
+"""Greedy generation with a KV cache (K12) for the causal-LM families.
+
+Reference: HF ``model.generate(**enc, max_new_tokens=16)`` on distilgpt2 in
+the lab generation probe (`run_labs45_tiny_final.sbatch:66-89`, SURVEY
+§3.5 / C42) and FLAN-T5 generation in the RAG lab.  Semantics kept from HF
+greedy search: left-padded batches, positions from the attention mask
+(GPT-2: cumsum(mask)-1; OPT: the same + offset 2), a finished row keeps
+emitting ``pad_token_id`` after ``eos_token_id``, stop when every row is
+finished.
+
+MI355X design: one preallocated cache per layer ``[B, H, Tmax, hd]`` (16-bit,
+HBM-resident — 288 GB makes Tmax = context limit affordable), prefill runs
+the normal block path (flash attention when unpadded) and stores K/V once;
+every decode step is the fused block path with the attention replaced by
+the ``decode_attn`` HIP kernel, which appends the new K/V in the same
+launch.  CPU tensors run the same algorithm with torch ops (the oracle).
+"""
+import torch
+
+from ..ops import reference as ref
+
+
+class KVCache:
+    def __init__(self, n_layers, B, H, Tmax, hd, dtype, device):
+        shape = (B, H, Tmax, hd)
+        self.k = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.v = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.Tmax = Tmax
+
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in self.k + self.v)
+
+
+def _split_heads(x, B, S, H, hd):
+    return x.view(B, S, H, hd).transpose(1, 2)
+
+
+def _prefill_attn(cache, li, B, S, H, hd, start, fused):
+    """attn(qkv [B,S,3d]) -> o [B,S,d]; stores K/V rows [0, S) of layer li."""
+    d = H * hd
+    scale = hd ** -0.5
+
+    def attn(qkv):
+        qkv3 = qkv.reshape(B, S, 3 * d)
+        q = _split_heads(qkv3[..., :d], B, S, H, hd)
+        k = _split_heads(qkv3[..., d:2 * d], B, S, H, hd)
+        v = _split_heads(qkv3[..., 2 * d:], B, S, H, hd)
+        cache.k[li][:, :, :S].copy_(k)
+        cache.v[li][:, :, :S].copy_(v)
+        if start is None and fused:
+            from ..ops.attention import causal_attention
+            return causal_attention(qkv3, B, S, H, hd, scale=scale)
+        valid = None
+        if start is not None:
+            valid = torch.arange(S, device=qkv.device)[None, :] >= start[:, None]
+        if fused:  # padded prompt on GPU: SDPA with an explicit causal & key mask (one-off prefill)
+            m = torch.ones(S, S, dtype=torch.bool, device=qkv.device).tril()[None, None]
+            if valid is not None:
+                m = m & valid[:, None, None, :]
+            o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=m, scale=scale)
+            o = torch.nan_to_num(o)
+        else:
+            o = ref.attention(q, k, v, causal=True, key_padding=valid, scale=scale)
+        return o.transpose(1, 2).reshape(B, S, d)
+
+    return attn
+
+
+def _decode_attn(cache, li, B, H, hd, t, start, start_i32, fused):
+    d = H * hd
+    scale = hd ** -0.5
+
+    def attn(qkv):
+        if fused:
+            from ..ops import kernels as K
+            o = K.decode_attn(qkv.reshape(B, 3 * d).contiguous(), cache.k[li], cache.v[li], t, scale, start_i32)
+            return o.view(B, 1, d)
+        qkv3 = qkv.reshape(B, 3 * d)
+        q = qkv3[:, :d].view(B, H, 1, hd)
+        cache.k[li][:, :, t] = qkv3[:, d:2 * d].view(B, H, hd)
+        cache.v[li][:, :, t] = qkv3[:, 2 * d:].view(B, H, hd)
+        k, v = cache.k[li][:, :, :t + 1], cache.v[li][:, :, :t + 1]
+        valid = None
+        if start is not None:
+            valid = torch.arange(t + 1, device=qkv.device)[None, :] >= start[:, None]
+        o = ref.attention(q, k, v, causal=False, key_padding=valid, scale=scale)
+        return o.transpose(1, 2).reshape(B, 1, d)
+
+    return attn
+
+
+def _run_blocks(model, h, attn_for_layer, fused):
+    for li, blk in enumerate(model.blocks()):
+        s = blk.site_seeds(0, 0)  # eval: no dropout is drawn
+        if fused:
+            h = blk.forward_fused(h, s, False, attn=attn_for_layer(li))
+        else:
+            h = blk.forward_ref(h, s, False, attn=attn_for_layer(li))
+    return h
+
+
+def _heads(model):
+    blk = model.blocks()[0]
+    a = getattr(blk, "attn", None) or getattr(blk, "self_attn")
+    return a.n_head, a.head_dim
+
+
+@torch.no_grad()
+def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token_id=None, pad_token_id=None,
+             max_length=None):
+    """Greedy decoding.  input_ids [B, S0] (left-padded if ``attention_mask`` has zeros).
+
+    Returns [B, S0 + n_generated] token ids (HF ``generate`` output layout)."""
+    model.eval()
+    dev = input_ids.device
+    B, S0 = input_ids.shape
+    cfg = model.config
+    eos = cfg.eos_token_id if eos_token_id is None else eos_token_id
+    pad = getattr(cfg, "pad_token_id", eos) if pad_token_id is None else pad_token_id
+    if max_length is not None:
+        max_new_tokens = max(0, min(max_new_tokens, max_length - S0))
+    if attention_mask is None:
+        attention_mask = torch.ones_like(input_ids)
+    lens = attention_mask.sum(1)
+    start = (S0 - lens)
+    if bool((attention_mask != (torch.arange(S0, device=dev)[None, :] >= start[:, None]).long()).any()):
+        raise ValueError("generate expects left padding (HF padding_side='left')")
+    padded = bool((start > 0).any())
+    start_t = start if padded else None
+    start_i32 = start.to(torch.int32).contiguous() if padded else None
+    fused = model._use_fused(input_ids)
+    H, hd = _heads(model)
+    L = len(model.blocks())
+    dtype = model.tied_embedding().dtype
+    cache = KVCache(L, B, H, S0 + max_new_tokens, hd, dtype, dev)
+
+    # prefill
+    pos = (torch.cumsum(attention_mask, 1) - 1).clamp(min=0) * attention_mask
+    h = model.embed_at(input_ids, pos)
+    h = _run_blocks(model, h, lambda li: _prefill_attn(cache, li, B, S0, H, hd, start_t, fused), fused)
+    logits = model.head_logits(h[:, -1:])
+    nxt = logits[:, -1].float().argmax(-1)
+    out = [input_ids]
+    done = torch.zeros(B, dtype=torch.bool, device=dev)
+    for i in range(max_new_tokens):
+        nxt = torch.where(done, torch.full_like(nxt, pad), nxt)
+        out.append(nxt[:, None])
+        if eos is not None:
+            done = done | (nxt == eos)
+        if i == max_new_tokens - 1 or (eos is not None and bool(done.all())):
+            break
+        t = S0 + i
+        pos = (lens + i)[:, None]
+        h = model.embed_at(nxt[:, None], pos)
+        h = _run_blocks(model, h, lambda li: _decode_attn(cache, li, B, H, hd, t, start_t, start_i32, fused), fused)
+        nxt = model.head_logits(h)[:, -1].float().argmax(-1)
+    return torch.cat(out, 1)
+
+
+@torch.no_grad()
+def generate_nocache(model, input_ids, max_new_tokens=16):
+    """Oracle: re-run the full forward for every new token (unpadded input only)."""
+    ids = input_ids
+    for _ in range(max_new_tokens):
+        logits = model(input_ids=ids)["logits"]
+        ids = torch.cat([ids, logits[:, -1].float().argmax(-1, keepdim=True)], 1)
+    return ids

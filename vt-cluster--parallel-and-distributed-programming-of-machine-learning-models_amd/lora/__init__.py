@@ -97,8 +97,9 @@ def lora_parameters(model: nn.Module):
 class LoraArena:
     """Flat fp32 storage for all LoRA params + grads (see module doc)."""
 
-    def __init__(self, model: nn.Module, device=None, align: int = 64, shards: int = 1):
-        self.named = lora_parameters(model)
+    def __init__(self, model: nn.Module, device=None, align: int = 64, shards: int = 1, named=None):
+        # ``named``: train an explicit parameter list instead (full fine-tuning, e.g. the tiny BERT lab)
+        self.named = list(named) if named is not None else lora_parameters(model)
         if not self.named:
             raise ValueError("model has no LoRA parameters (call mift.lora.inject first)")
         device = device or self.named[0][1].device

@@ -54,6 +54,26 @@ class CausalLMBase(nn.Module):
     def num_layers(self):
         return self.config.num_layers()
 
+    # ---- generation hooks (mift.infer.generate) ----
+    POS_OFFSET = 0
+
+    def embed_at(self, ids, pos):
+        """Token + learned-position embedding for explicit positions (no dropout)."""
+        wte, wpe = self.embedding_tables()
+        if self._use_fused(ids):
+            from ..ops import kernels as K
+            B, S = ids.shape
+            return K.embed(ids.contiguous(), wte.weight, wpe.weight, pos=pos.contiguous(),
+                           pos_offset=self.POS_OFFSET).view(B, S, -1)
+        return wte(ids) + wpe(pos + self.POS_OFFSET)
+
+    def head_logits(self, h):
+        """[B, S, d] -> [B, S, V] through the final LayerNorm and the tied head."""
+        if self._use_fused(h):
+            from ..ops import fused as F
+            return F.lm_head_logits(h, self.final_norm(), self.lm_weight_padded()[0], self.config.vocab_size)
+        return self.final_norm()(h) @ self.tied_embedding().t()
+
     def stage_parameters(self):
         """(name, tensor) of everything this stage materialised (for memory reports)."""
         return list(self.named_parameters())

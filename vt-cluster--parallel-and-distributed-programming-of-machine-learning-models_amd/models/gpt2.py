@@ -94,20 +94,24 @@ class GPT2Block(nn.Module):
         return {k: seed_for(base, step, s + i) for i, k in
                 enumerate(["attn", "attn_out", "mlp_out", "lora_attn", "lora_proj", "lora_mlp"])}
 
-    def forward_ref(self, h, seeds, training, key_valid=None):
-        """h: [B, S, d] (reference path)."""
+    def forward_ref(self, h, seeds, training, key_valid=None, attn=None):
+        """h: [B, S, d] (reference path).  ``attn(qkv) -> o`` overrides the attention
+        (KV-cache decode / padded prefill in mift.infer.generate)."""
         B, S, d = h.shape
         H, hd = self.attn.n_head, self.attn.head_dim
         cfg = self.cfg
         a = self.ln_1(h)
         qkv = self.attn.c_attn(a, seeds["lora_attn"])
-        q, k, v = qkv.split(d, dim=-1)
-        q = q.view(B, S, H, hd).transpose(1, 2)
-        k = k.view(B, S, H, hd).transpose(1, 2)
-        v = v.view(B, S, H, hd).transpose(1, 2)
-        o = ref.attention(q, k, v, causal=True, key_padding=key_valid, scale=hd ** -0.5,
-                          dropout_p=cfg.attn_pdrop if training else 0.0, seed=seeds["attn"])
-        o = o.transpose(1, 2).reshape(B, S, d)
+        if attn is not None:
+            o = attn(qkv)
+        else:
+            q, k, v = qkv.split(d, dim=-1)
+            q = q.view(B, S, H, hd).transpose(1, 2)
+            k = k.view(B, S, H, hd).transpose(1, 2)
+            v = v.view(B, S, H, hd).transpose(1, 2)
+            o = ref.attention(q, k, v, causal=True, key_padding=key_valid, scale=hd ** -0.5,
+                              dropout_p=cfg.attn_pdrop if training else 0.0, seed=seeds["attn"])
+            o = o.transpose(1, 2).reshape(B, S, d)
         y = self.attn.c_proj(o, seeds["lora_proj"])
         if training and cfg.resid_pdrop > 0:
             y = ref.dropout(y, cfg.resid_pdrop, seeds["attn_out"])
@@ -118,6 +122,25 @@ class GPT2Block(nn.Module):
         if training and cfg.resid_pdrop > 0:
             y2 = ref.dropout(y2, cfg.resid_pdrop, seeds["mlp_out"])
         return h + y2
+
+    def forward_fused(self, h, seeds, training, kv_len=None, attn=None):
+        """Fused HIP path: LN+c_attn(+LoRA) -> attention -> c_proj(+LoRA)+dropout+residual
+        -> LN+c_fc+gelu_new -> c_proj(+LoRA)+dropout+residual (mift.ops.fused)."""
+        from ..ops import fused as F
+        from ..ops.attention import causal_attention
+        cfg = self.cfg
+        B, S, d = h.shape
+        H, hd = self.attn.n_head, self.attn.head_dim
+        qkv = F.ln_linear(h, self.ln_1, self.attn.c_attn, seeds["lora_attn"], training)
+        if attn is not None:
+            o = attn(qkv)
+        else:
+            o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5, dropout_p=cfg.attn_pdrop if training else 0.0,
+                                 seed=seeds["attn"], kv_len=kv_len)
+        h = F.linear_residual(o, h, self.attn.c_proj, cfg.resid_pdrop, seeds["attn_out"], seeds["lora_proj"],
+                              training)
+        return F.mlp(h, self.ln_2, self.mlp.c_fc, self.mlp.c_proj, act=1, p=cfg.resid_pdrop, seed=seeds["mlp_out"],
+                     seed_l1=0, seed_l2=seeds["lora_mlp"], training=training)
 
 
 class GPT2LMHeadModel(CausalLMBase):
@@ -155,6 +178,12 @@ class GPT2LMHeadModel(CausalLMBase):
 
     def tied_embedding(self):
         return self.transformer.wte.weight
+
+    def embedding_tables(self):
+        return self.transformer.wte, self.transformer.wpe
+
+    def final_norm(self):
+        return self.transformer.ln_f
 
     # ---- reference path pieces ----
     def embed_ref(self, input_ids, attention_mask=None):

@@ -120,20 +120,26 @@ class OPTDecoderLayer(nn.Module):
         s = 100 + 10 * self.idx
         return {k: seed_for(base, step, s + i) for i, k in enumerate(self.SITES)}
 
-    def forward_ref(self, h, seeds, training, key_valid=None):
-        """h: [B, S, d] (reference path).  One LoRA-dropout seed for q/k/v (see MultiAdapterOps)."""
+    def forward_ref(self, h, seeds, training, key_valid=None, attn=None):
+        """h: [B, S, d] (reference path).  One LoRA-dropout seed for q/k/v (see MultiAdapterOps).
+        ``attn(qkv [B,S,3d]) -> o [B,S,d]`` overrides the attention (KV-cache decode)."""
         cfg = self.cfg
         B, S, d = h.shape
         H, hd = self.self_attn.n_head, self.self_attn.head_dim
         at = self.self_attn
         a = self.self_attn_layer_norm(h)
         sl = seeds["lora_attn"]
-        q = at.q_proj(a, sl).view(B, S, H, hd).transpose(1, 2)
-        k = at.k_proj(a, sl).view(B, S, H, hd).transpose(1, 2)
-        v = at.v_proj(a, sl).view(B, S, H, hd).transpose(1, 2)
-        o = ref.attention(q, k, v, causal=True, key_padding=key_valid, scale=hd ** -0.5,
-                          dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"])
-        y = at.out_proj(o.transpose(1, 2).reshape(B, S, d), seeds["lora_proj"])
+        q, k, v = at.q_proj(a, sl), at.k_proj(a, sl), at.v_proj(a, sl)
+        if attn is not None:
+            o = attn(torch.cat([q, k, v], -1))
+        else:
+            q = q.view(B, S, H, hd).transpose(1, 2)
+            k = k.view(B, S, H, hd).transpose(1, 2)
+            v = v.view(B, S, H, hd).transpose(1, 2)
+            o = ref.attention(q, k, v, causal=True, key_padding=key_valid, scale=hd ** -0.5,
+                              dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"])
+            o = o.transpose(1, 2).reshape(B, S, d)
+        y = at.out_proj(o, seeds["lora_proj"])
         if training and cfg.dropout > 0:
             y = ref.dropout(y, cfg.dropout, seeds["attn_out"])
         h = h + y
@@ -144,7 +150,7 @@ class OPTDecoderLayer(nn.Module):
             y2 = ref.dropout(y2, cfg.dropout, seeds["mlp_out"])
         return h + y2
 
-    def forward_fused(self, h, seeds, training, kv_len=None):
+    def forward_fused(self, h, seeds, training, kv_len=None, attn=None):
         from ..ops import fused as F
         from ..ops.attention import causal_attention
         cfg = self.cfg
@@ -156,8 +162,12 @@ class OPTDecoderLayer(nn.Module):
         else:  # adapters too wide for one shared K-extension: three projections
             qkv = torch.cat([F.ln_linear(h, self.self_attn_layer_norm, l, seeds["lora_attn"], training)
                              for l in (at.q_proj, at.k_proj, at.v_proj)], -1)
-        o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5,
-                             dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"], kv_len=kv_len)
+        if attn is not None:
+            o = attn(qkv)
+        else:
+            o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5,
+                                 dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"],
+                                 kv_len=kv_len)
         h = F.linear_residual(o, h, at.out_proj, cfg.dropout, seeds["attn_out"], seeds["lora_proj"], training)
         return F.mlp(h, self.final_layer_norm, self.fc1, self.fc2, act=2, p=cfg.dropout, seed=seeds["mlp_out"],
                      seed_l1=seeds["lora_fc1"], seed_l2=seeds["lora_fc2"], training=training)
@@ -207,8 +217,16 @@ class OPTForCausalLM(CausalLMBase):
         init_normal_(self, self.config.init_std, seed=seed)
         return self
 
+    POS_OFFSET = 2
+
     def tied_embedding(self):
         return self.model.decoder.embed_tokens.weight
+
+    def embedding_tables(self):
+        return self.model.decoder.embed_tokens, self.model.decoder.embed_positions
+
+    def final_norm(self):
+        return self.model.decoder.final_layer_norm
 
     def blocks(self):
         return [b for b in self.model.decoder.layers if isinstance(b, OPTDecoderLayer)]

@@ -68,3 +68,8 @@ def pack_lora(A, B, a_scale, dtype):
 
 def xent(logits, labels, V, ignore_index=-100, write_grad=True):
     return C().xent_fwd_bwd(logits, labels, int(V), int(ignore_index), bool(write_grad))
+
+
+def decode_attn(qkv, kcache, vcache, t, scale, start=None):
+    """o [B, H*hd] for the token at position t; writes its k/v into the caches."""
+    return C().decode_attn(qkv, kcache, vcache, int(t), float(scale), start)

@@ -57,10 +57,12 @@ class TrainConfig:
     recompute: bool = False
     shuffle: bool = False
     zero_stage: int = 0                # 1: shard AdamW state over the DP group (mift.parallel.zero)
+    trainable: str = "lora"            # lora | all (full fine-tuning: the tiny-BERT lab)
+    logging_first_step: bool = False
 
 
 class Trainer:
-    def __init__(self, model, batcher, cfg: TrainConfig, ctx=None, callbacks=()):
+    def __init__(self, model, batcher, cfg: TrainConfig, ctx=None, callbacks=(), epoch_callbacks=()):
         self.model, self.batcher, self.cfg, self.ctx = model, batcher, cfg, ctx
         self.rank = ctx.rank if ctx else 0
         self.device = ctx.device if ctx else torch.device("cpu")
@@ -68,8 +70,11 @@ class Trainer:
         self.dp = ctx.dp if ctx else 1
         self.pp = ctx.pp if ctx else 1
         self.zero = cfg.zero_stage >= 1 and self.dp > 1
-        self.arena = LoraArena(model, device=self.device, shards=self.dp if self.zero else 1)
-        if self.device.type == "cuda" and getattr(model, "fused", False):
+        named = None
+        if cfg.trainable == "all":
+            named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        self.arena = LoraArena(model, device=self.device, shards=self.dp if self.zero else 1, named=named)
+        if self.device.type == "cuda" and getattr(model, "fused", False) and named is None:
             from ..lora.pack import attach
             from ..ops.dispatch import use_kernels
             if use_kernels(self.arena.param):
@@ -102,14 +107,20 @@ class Trainer:
         self.total_steps = total
         self.sched = linear_schedule(cfg.lr, total, cfg.warmup_steps)
         self.global_step = 0
-        self.callbacks = list(callbacks)
+        self.callbacks = list(callbacks)              # (trainer, log record) at logging steps
+        self.epoch_callbacks = list(epoch_callbacks)  # (trainer, epoch) at each epoch end (eval)
         self.history = []
-        model.recompute = cfg.recompute
+        if hasattr(model, "recompute"):
+            model.recompute = cfg.recompute
         self._ctrl = ctx.ctrl_group if ctx else None
 
     # ------------------------------------------------------------------
     def _global_tokens(self, mbs):
-        n = sum(int((mb["labels"][:, 1:] != -100).sum()) for mb in mbs)
+        count = getattr(self.model, "count_targets", None)
+        if count is not None:  # e.g. sequence classification: one target per row
+            n = sum(count(mb["labels"]) for mb in mbs)
+        else:  # causal LM: shifted label tokens
+            n = sum(int((mb["labels"][:, 1:] != -100).sum()) for mb in mbs)
         if self.dp > 1 and dist.is_initialized():
             t = torch.tensor([n], dtype=torch.float64)
             dist.all_reduce(t, group=self._dp_ctrl_group())
@@ -201,7 +212,9 @@ class Trainer:
             for mbs in self.batcher.epoch(epoch, start_step=max(0, skip)):
                 loss_sum, ntok = self.train_step(mbs)
                 maybe_inject(self.rank, self.global_step, "step")
-                if cfg.step_log != "none" or (cfg.logging_steps and self.global_step % cfg.logging_steps == 0):
+                log_now = bool(cfg.logging_steps) and (self.global_step % cfg.logging_steps == 0 or
+                                                       (cfg.logging_first_step and self.global_step == 1))
+                if cfg.step_log != "none" or log_now:
                     if sync_dev:
                         torch.cuda.synchronize()
                     now = time.perf_counter()
@@ -214,7 +227,7 @@ class Trainer:
                         sps = samples / max(dt, 1e-9)
                         seq = mbs[0]["input_ids"].shape[1]
                         print(lab_step_line(self.rank, self.global_step, dt * 1000, sps, sps * seq), flush=True)
-                if cfg.logging_steps and self.global_step % cfg.logging_steps == 0:
+                if log_now:
                     st = self.opt.stats()
                     rec = {"loss": self._loss_for_log(loss_sum) / max(1, ntok),
                            "grad_norm": st["grad_norm"], "learning_rate": self.sched(self.global_step),
@@ -229,6 +242,8 @@ class Trainer:
                 if self.global_step >= self.total_steps:
                     done = True
                     break
+            for cb in self.epoch_callbacks:
+                cb(self, epoch)
             epoch += 1
             start_step = epoch * self.steps_per_epoch
             if epoch * self.steps_per_epoch >= self.total_steps:
@@ -241,10 +256,14 @@ class Trainer:
     def save_checkpoint(self):
         """``checkpoint-<step>/``: adapter + optimizer + rng + trainer_state (+rotation)."""
         out = os.path.join(self.cfg.output_dir, f"checkpoint-{self.global_step}")
-        state = self.adapter_state()
+        full = self.cfg.trainable == "all"
+        state = {} if full else self.adapter_state()
         if self.rank == 0:
             os.makedirs(out, exist_ok=True)
-            save_adapter(out, state, self.model.lora_config)
+            if full:
+                self.model.save_pretrained(out)
+            else:
+                save_adapter(out, state, self.model.lora_config)
             with open(os.path.join(out, "trainer_state.json"), "w") as f:
                 json.dump({"global_step": self.global_step, "max_steps": self.total_steps,
                            "steps_per_epoch": self.steps_per_epoch, "log_history": self.history,
@@ -284,8 +303,12 @@ class Trainer:
             if not cks:
                 return 0
             path = os.path.join(self.cfg.output_dir, max(cks, key=lambda d: int(d.split("-")[1])))
-        from ..lora import load_adapter
-        load_adapter(self.model, path)
+        if self.cfg.trainable == "all":
+            from ..models import load_hf_weights
+            load_hf_weights(self.model, path)
+        else:
+            from ..lora import load_adapter
+            load_adapter(self.model, path)
         self.opt.load_state_dict(torch.load(os.path.join(path, self._opt_file()), weights_only=True))
         with open(os.path.join(path, "trainer_state.json")) as f:
             st = json.load(f)
