@@ -31,6 +31,8 @@ TRAIN_FALLBACK_OFFSET = 2048
 
 
 def cache_roots():
+    if os.environ.get("MIFT_AGNEWS") == "synthetic":
+        return []
     roots = [os.environ.get("MIFT_HF_CACHE"), os.environ.get("HF_HOME"), os.path.join(os.getcwd(), ".hf_cache"),
              os.path.expanduser("~/.cache/huggingface"), "/root/reference/.hf_cache"]
     return [r for r in roots if r and os.path.isdir(r)]
