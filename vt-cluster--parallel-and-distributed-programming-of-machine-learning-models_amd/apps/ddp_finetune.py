@@ -62,6 +62,7 @@ def build_argparser(defaults=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--step_log", choices=["p1", "lab", "none"], default="p1")
     ap.add_argument("--no_save", action="store_true")
+    ap.add_argument("--run_name", type=str, default=None, help="fixed run dir name (resume across jobs)")
     if defaults:
         ap.set_defaults(**defaults)
     return ap
@@ -127,7 +128,7 @@ def main(argv=None, defaults=None):
     mb, acc = (args.batch * args.accum, 1) if fold else (args.batch, args.accum)
     stamp = datetime.datetime.now().strftime("%Y%m%d-%H%M%S")
     base = args.model.split("/")[-1]
-    run_name = f"{base}_lora_{args.dataset}_N{world}_{stamp}"
+    run_name = args.run_name or f"{base}_lora_{args.dataset}_N{world}_{stamp}"
     save_dir = os.path.join(args.out_root, run_name)
     batcher = MicroBatcher(ds, mb, acc, rank=ctx.dp_rank, world=ctx.dp, mode="strided")
     tcfg = TrainConfig(epochs=args.epochs, batch=mb, accum=acc, lr=args.lr, precision=precision,

@@ -71,6 +71,7 @@ class DistContext:
     dp_group: Optional[object] = None
     pp_group: Optional[object] = None
     pp_ranks: List[int] = field(default_factory=list)
+    timeout: Optional[object] = None        # collective timeout (watchdog) for every group
     dp_ranks: List[int] = field(default_factory=list)
 
     @property
@@ -129,7 +130,11 @@ def init(pp: Optional[int] = None, backend: Optional[str] = None, timeout_s: Opt
         device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
-    timeout = datetime.timedelta(seconds=timeout_s or int(os.environ.get("GLOO_SOCKET_TIMEOUT", "1800")))
+    timeout = datetime.timedelta(seconds=timeout_s or int(os.environ.get("MIFT_COMM_TIMEOUT",
+                                                                         os.environ.get("GLOO_SOCKET_TIMEOUT", "1800"))))
+    # RCCL watchdog: a collective that exceeds `timeout` aborts the communicator and
+    # tears the process down (non-zero exit -> torchrun / srun --kill-on-bad-exit end the job)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
         kw = dict(backend=backend, init_method="env://", rank=rank, world_size=world, timeout=timeout)
         if backend == "nccl":
@@ -141,6 +146,7 @@ def init(pp: Optional[int] = None, backend: Optional[str] = None, timeout_s: Opt
     pp = pp or int(os.environ.get("PIPELINE_PARALLEL_SIZE", "1") or 1)
     if pp < 1 or world % pp != 0:
         raise ValueError(f"pipeline size {pp} must divide world size {world}")
+    ctx.timeout = timeout
     build_grid(ctx, pp)
     _CTX = ctx
     if verbose:
@@ -163,12 +169,12 @@ def build_grid(ctx: DistContext, pp: int):
     # every rank must create every group in the same order
     for r in range(dp):
         ranks = list(range(r * pp, (r + 1) * pp))
-        g = dist.new_group(ranks) if pp > 1 and world > 1 else None
+        g = dist.new_group(ranks, timeout=ctx.timeout) if pp > 1 and world > 1 else None
         if ctx.rank in ranks:
             ctx.pp_group, ctx.pp_ranks = g, ranks
     for s in range(pp):
         ranks = list(range(s, world, pp))
-        g = dist.new_group(ranks) if dp > 1 and world > 1 else None
+        g = dist.new_group(ranks, timeout=ctx.timeout) if dp > 1 and world > 1 else None
         if ctx.rank in ranks:
             ctx.dp_group, ctx.dp_ranks = g, ranks
     if ctx.dp_group is None and dp == 1 and world == 1:

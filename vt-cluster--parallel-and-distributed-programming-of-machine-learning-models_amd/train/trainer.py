@@ -138,7 +138,7 @@ class Trainer:
                     groups = {}
                     for s in range(self.ctx.pp):
                         ranks = list(range(s, self.ctx.world, self.ctx.pp))
-                        groups[s] = dist.new_group(ranks, backend="gloo")
+                        groups[s] = dist.new_group(ranks, backend="gloo", timeout=self.ctx.timeout)
                     self._dpc = groups[self.ctx.pp_rank]
         return self._dpc
 

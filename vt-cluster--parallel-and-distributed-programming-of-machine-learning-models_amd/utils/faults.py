@@ -1,6 +1,6 @@
 """Fault injection for teardown / resume tests (SURVEY §5.3 plan).
 
-``MIFT_FAULT=rank:step:kind[:where]`` — on global rank ``rank`` when the
+``MIFT_FAULT=rank:step:kind[:where]`` — on global rank ``rank`` (``*`` = all) when the
 trainer reaches optimizer step ``step``: ``raise`` (RuntimeError), ``exit``
 (os._exit(17), like a killed node) or ``hang`` (sleep until the collective
 timeout / watchdog fires).  ``where`` is ``step`` (after the optimizer
@@ -11,6 +11,7 @@ import os
 import time
 
 EXIT_CODE = 17
+_fired = False
 
 
 def parse(spec: str):
@@ -18,16 +19,18 @@ def parse(spec: str):
     if len(parts) < 3:
         raise ValueError(f"bad MIFT_FAULT spec {spec!r}")
     where = parts[3] if len(parts) > 3 else "step"
-    return int(parts[0]), int(parts[1]), parts[2], where
+    return (None if parts[0] == "*" else int(parts[0])), int(parts[1]), parts[2], where
 
 
 def maybe_inject(rank: int, step: int, where: str = "step"):
     spec = os.environ.get("MIFT_FAULT")
     if not spec:
         return
+    global _fired
     r, s, kind, w = parse(spec)
-    if r != rank or s != step or w != where:
+    if _fired or (r is not None and r != rank) or s != step or w != where:
         return
+    _fired = True  # once per process (several micro-batches share a step number)
     print(f"[FAULT] injecting {kind} on rank {rank} at step {step} ({where})", flush=True)
     if kind == "raise":
         raise RuntimeError(f"injected fault on rank {rank} step {step}")
