@@ -46,22 +46,24 @@ GEMM_SHAPES = [
     ("mlp.c_proj.dgrad", 8192, 3072, 768),
     ("lm_head.fwd", 8192, 50304, 768),
     ("lm_head.dgrad", 8192, 768, 50304),
-    # OPT-2.7B, 4x512 tokens per micro-batch
-    ("opt.qkv.fwd", 2048, 7680, 2560),
-    ("opt.fc1.fwd", 2048, 10240, 2560),
-    ("opt.fc2.fwd", 2048, 2560, 10240),
     ("square4k", 4096, 4096, 4096),
+]
+OPT_SHAPES = [  # OPT-2.7B, 8x512 tokens per micro-batch (every distinct GEMM of a layer)
+    ("opt.qkv.fwd", 4096, 7680, 2560), ("opt.out.fwd", 4096, 2560, 2560), ("opt.fc1.fwd", 4096, 10240, 2560),
+    ("opt.fc2.fwd", 4096, 2560, 10240), ("opt.qkv.dgrad", 4096, 2560, 7680), ("opt.fc1.dgrad", 4096, 2560, 10240),
+    ("opt.fc2.dgrad", 4096, 10240, 2560), ("opt.lm_head.fwd", 4096, 50304, 2560),
+    ("opt.fc2.fwd.M2k", 2048, 2560, 10240), ("opt.fc2.fwd.M16k", 16384, 2560, 10240),
 ]
 
 
-def bench_gemm(results):
+def bench_gemm(results, shapes=None, dtype=torch.bfloat16):
     import mift._C as C
-    for name, M, N, K in GEMM_SHAPES:
-        a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-        b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    for name, M, N, K in shapes or GEMM_SHAPES:
+        a = torch.randn(M, K, device="cuda", dtype=dtype)
+        b = torch.randn(N, K, device="cuda", dtype=dtype)
         fl = 2.0 * M * N * K
         row = {"name": name, "M": M, "N": N, "K": K}
-        for tile in (0, 1, 2, 3, 4):
+        for tile in (0, 1, 2, 3, 4, 5, 6):
             t = timeit(lambda: C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, tile, None, None, 0.0, 0))
             row[f"mift_t{tile}_ms"] = round(t, 4)
             row[f"mift_t{tile}_tflops"] = round(fl / t / 1e9, 1)
@@ -95,7 +97,8 @@ def main():
     assert mift.kernels_available(), mift._ext.error()
     results = []
     for k in a.only.split(","):
-        {"gemm": bench_gemm, "ln": bench_ln}[k](results)
+        {"gemm": bench_gemm, "ln": bench_ln,
+         "opt": lambda r: bench_gemm(r, OPT_SHAPES, torch.float16)}[k](results)
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
         with open(a.json, "w") as f:

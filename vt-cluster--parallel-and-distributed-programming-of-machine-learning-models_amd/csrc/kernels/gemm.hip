@@ -338,6 +338,8 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
 //   2: 128x64,  4 waves (2x2), 3-stage ring (72 KiB, 2 blocks/CU)  — N ~ 768
 //   3: 128x128, 4 waves (2x2), 2-stage ring (64 KiB, 2 blocks/CU)
 //   4: 64x64,   4 waves (2x2), 3-stage ring (48 KiB)               — tiny problems
+//   5: 256x256, 8 waves (2x4), 2-stage ring (128 KiB; C tile 132 KiB) — halves L2->CU bytes/MAC vs 128x128
+//   6: 128x256, 8 waves (2x4), 2-stage ring (96 KiB)
 template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
@@ -356,6 +358,8 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     case 1: launch_gemm<T, 256, 128, 4, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 2: launch_gemm<T, 128, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 3: launch_gemm<T, 128, 128, 2, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 5: launch_gemm<T, 256, 256, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 6: launch_gemm<T, 128, 256, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     default: launch_gemm<T, 64, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
   }
 }

@@ -58,27 +58,38 @@ MIFT_HD frag_t<T> masked_frag(const T* p, uint64_t seed, uint64_t idx0, uint32_t
 }
 
 // ------------------------------------------------------------------ lora_proj
+// Grid = (M/32 row blocks) x KS K-splits: with only M/32 row blocks (128 for
+// M = 4096) the kernel filled half of the 256 CUs and ran latency-bound; the
+// K-splits give >= ~1024 blocks.  KS > 1: every block adds its [32,32] fp32
+// partial into the zeroed workspace ``ws`` with atomics, and the LAST block of
+// a row block (per-row-block arrival counter after a release fence) converts
+// the finished sums to 16-bit — one launch, no second pass.
 template <typename T>
 __global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X, const T* __restrict__ W,
                                                         T* __restrict__ out, int M, int K, int ldx, float alpha,
-                                                        uint64_t seed, uint32_t thr, float inv_keep) {
+                                                        uint64_t seed, uint32_t thr, float inv_keep, int KS,
+                                                        float* __restrict__ ws, int* __restrict__ cnt) {
   __shared__ float red[4][32][33];
+  __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, fr = lane & 15;
-  const int m0 = blockIdx.x * 32;
+  const int mb = blockIdx.x / KS, kss = blockIdx.x % KS;
+  const int m0 = mb * 32;
   float4_ acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
   const int rows[2] = {min(m0 + fr, M - 1), min(m0 + 16 + fr, M - 1)};
-  const int nks = K / 32;
-  // each wave owns a contiguous K range; UNR k-steps of loads are issued
-  // back to back before their MFMAs (memory-level parallelism: this kernel is
-  // latency-bound, one 16-B load per lane per operand per k-step)
+  const int nks_all = K / 32;
+  const int per_blk = (nks_all + KS - 1) / KS;
+  const int kb0 = kss * per_blk, nks = min(nks_all, kb0 + per_blk);
+  // each wave owns a contiguous K range of the block's split; UNR k-steps of
+  // loads are issued back to back before their MFMAs (memory-level
+  // parallelism: one 16-B load per lane per operand per k-step)
   constexpr int UNR = 4;
-  const int per = (nks + 3) / 4;
-  const int kbeg = wave * per, kend = min(nks, kbeg + per);
+  const int per = (nks - kb0 + 3) / 4;
+  const int kbeg = kb0 + wave * per, kend = min(nks, kbeg + per);
   for (int ks0 = kbeg; ks0 < kend; ks0 += UNR) {
     short8 ra[UNR][2], rb[UNR][2];
 #pragma unroll
@@ -127,10 +138,30 @@ __global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X,
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wave][i * 16 + g * 4 + r][j * 16 + fr] = acc[i][j][r];
   __syncthreads();
+  if (KS == 1) {
+    for (int e = tid; e < 32 * 32; e += 256) {
+      const int r = e >> 5, c = e & 31;
+      const float v = (red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c]) * alpha;
+      if (m0 + r < M) out[(int64_t)(m0 + r) * 32 + c] = (T)v;
+    }
+    return;
+  }
   for (int e = tid; e < 32 * 32; e += 256) {
     const int r = e >> 5, c = e & 31;
-    const float v = (red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c]) * alpha;
-    if (m0 + r < M) out[(int64_t)(m0 + r) * 32 + c] = (T)v;
+    if (m0 + r < M) atomicAdd(ws + (int64_t)(m0 + r) * 32 + c, red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c]);
+  }
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(cnt + mb, 1) == KS - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (int e = tid; e < 32 * 32; e += 256) {
+    const int r = e >> 5, c = e & 31;
+    if (m0 + r < M) {
+      const float v = __hip_atomic_load(ws + (int64_t)(m0 + r) * 32 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      out[(int64_t)(m0 + r) * 32 + c] = (T)(v * alpha);
+    }
   }
 }
 
@@ -269,15 +300,26 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const uint32_t thr = mift_thr16(p);
   const float ik = p > 0 ? mift_inv_keep(p) : 1.f;
-  const int grid = (M + 31) / 32;
+  const int mblocks = (M + 31) / 32, nks = K / 32;
+  // K-splits so the launch covers the chip (>= ~1024 blocks), >= 4 k-steps (one per wave) each
+  const int KS = std::max(1, std::min(std::max(1, nks / 4), (1024 + mblocks - 1) / mblocks));
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  at::Tensor wsb;
+  if (KS > 1) {
+    wsb = at::zeros({(int64_t)M * 32 + mblocks}, x.options().dtype(at::kFloat));
+    ws = wsb.data_ptr<float>();
+    cnt = reinterpret_cast<int*>(ws + (int64_t)M * 32);
+  }
+  const int grid = mblocks * KS;
   if (x.scalar_type() == at::kBFloat16)
     lora_proj_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)x.data_ptr(), (const bf16*)w.data_ptr(),
                                                  (bf16*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                 (uint64_t)seed, thr, ik);
+                                                 (uint64_t)seed, thr, ik, KS, ws, cnt);
   else
     lora_proj_kernel<fp16><<<grid, 256, 0, st>>>((const fp16*)x.data_ptr(), (const fp16*)w.data_ptr(),
                                                  (fp16*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                 (uint64_t)seed, thr, ik);
+                                                 (uint64_t)seed, thr, ik, KS, ws, cnt);
   return out;
 }
 
