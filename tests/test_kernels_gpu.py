@@ -217,3 +217,25 @@ def test_gemm_ext_masked():
     out = C.gemm_nt(a, b, None, a2, b2, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.05, 1234)[0]
     exp = a.float() @ b.float().t() + ref.dropout(a2.float() @ b2.float().t(), 0.05, 1234)
     torch.testing.assert_close(out.float(), exp, atol=5e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("M,N,K", [(4096, 2560, 2560), (1000, 2304, 768), (8192, 768, 3072)])
+def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):
+    """Every tile config incl. the split-K ragged-wave tail (triggered for these shapes on 256 CUs)
+    with the full epilogue: bias, LoRA K-ext, gelu, pre-activation, dropout, residual."""
+    C = _C()
+    torch.manual_seed(11)
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
+    b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    out, pre = C.gemm_nt(a, b, bias, a2, b2, 1, None, res, 0.1, 5, True, 1.0, None, tile, None, None, 0.0, 0)
+    exp, exp_pre = ref.gemm_nt(a, b, bias, a2, b2, 1, None, res, 0.1, 5, True)
+    torch.testing.assert_close(pre.float(), exp_pre.float(), atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(out.float(), exp.float(), atol=8e-2, rtol=3e-2)
+    # repeated calls re-use the self-re-arming tile counters
+    out2 = C.gemm_nt(a, b, bias, a2, b2, 1, None, res, 0.1, 5, False, 1.0, None, tile, None, None, 0.0, 0)[0]
+    assert torch.equal(out, out2)

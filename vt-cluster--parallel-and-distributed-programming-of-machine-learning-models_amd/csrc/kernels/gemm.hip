@@ -69,6 +69,21 @@ struct EpiArgs {
   float ext_inv_keep;
 };
 
+// Split-K tail (second launch of a hybrid data-parallel + split-K GEMM): the
+// ragged last wave of tiles [tile0, tile0 + ntiles) is cut into gx k-chunks per
+// tile, one block per chunk.  Chunk blocks store fp32 partials and release a
+// per-tile counter; the last-chunk block acquires it (agent scope: chunks may
+// sit on different XCDs / L2s), reduces, runs the normal fused epilogue and
+// re-arms the counter.  It only waits for lower-index blocks, which the
+// in-order dispatcher started earlier, so it cannot deadlock even when RCCL
+// kernels hold some CUs.
+struct SkArgs {
+  int enabled;
+  int tile0, ntiles, gx;  // gx = k-splits per tile
+  float* ws;   // [ntiles * gx][BM*BN] fp32 partial slots (one per block)
+  int* flags;  // [ntiles] arrival counters, zero on entry and on exit
+};
+
 template <typename T>
 using frag_t = typename std::conditional<std::is_same<T, bf16>::value, bf16x8, fp16x8>::type;
 
@@ -102,11 +117,11 @@ MIFT_HD void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE>
+template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, bool SKM>
 __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                                 T* __restrict__ C, const T* __restrict__ A2,
                                                                 const T* __restrict__ B2, int M, int N, int K,
-                                                                int lda, int ldb, int ldc, EpiArgs ep) {
+                                                                int lda, int ldb, int ldc, EpiArgs ep, SkArgs sk) {
   constexpr int NW = NWM * NWN;
   constexpr int NT = NW * 64;
   constexpr int WM = BM / NWM, WN = BN / NWN;  // wave tile
@@ -123,17 +138,8 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / NWN, wn = wave % NWN;
 
-  // ---- XCD-aware bijective block remap (T1) ----
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
-  const int nblk = ntm * ntn;
-  int bid = blockIdx.x;
-  {
-    const int q = nblk / 8, r = nblk % 8;
-    const int xcd = bid % 8, loc = bid / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-  }
-  const int tm = bid / ntn, tn = bid % ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
+  int m0 = 0, n0 = 0;
 
   // per-lane staging coordinates: lane -> (row-in-8 = lane>>3, phys chunk = lane&7)
   const int srow = lane >> 3, spc = lane & 7;
@@ -160,158 +166,246 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   };
 
   float4_ acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-  // prologue: NSTAGE-1 tiles in flight
-#pragma unroll
-  for (int s = 0; s < NSTAGE - 1; ++s)
-    if (s < nk) stage(s, s * BK);
-
   const int fr = lane & 15;  // fragment row
   const int fq = lane >> 4;  // k sub-chunk (0..3)
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed <=> at most (#tiles issued after kt) * PER_STAGE pieces outstanding
-    if constexpr (NSTAGE >= 3) {
-      if (kt + 1 < nk) wait_vmcnt<PER_STAGE>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // everyone's pieces of kt landed; everyone done reading kt-1
-    asm volatile("" ::: "memory");  // no LDS access may move above the barrier
-    if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, (kt + NSTAGE - 1) * BK);
-    const char* As = smem + (kt % NSTAGE) * STAGE_BYTES;
-    const char* Bs = As + A_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int lc = kk * 4 + fq;
-      frag_t<T> af[TM], bfv[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int r = wm * WM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const frag_t<T>*>(As + r * ROWB + ((lc ^ (r & 7)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int r = wn * WN + j * 16 + fr;
-        bfv[j] = *reinterpret_cast<const frag_t<T>*>(Bs + r * ROWB + ((lc ^ (r & 7)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(bfv[j], af[i], acc[i][j]);
-    }
-  }
 
-  // ---- LoRA K-extension: one extra K=32 step from global (A2[M,32], B2[N,32]) ----
-  frag_t<T> af2[TM], bf2[TN];
-  const bool ext = A2 != nullptr;
-  if (ext) {
+  // acc = sum over k-tiles [kb, ke) of the (m0, n0) tile
+  auto mainloop = [&](int kb, int ke) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int r = min(m0 + wm * WM + i * 16 + fr, M - 1);
-      af2[i] = *reinterpret_cast<const frag_t<T>*>(A2 + (size_t)r * 32 + fq * 8);
-    }
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int r = min(n0 + wn * WN + j * 16 + fr, N - 1);
-      bf2[j] = *reinterpret_cast<const frag_t<T>*>(B2 + (size_t)r * 32 + fq * 8);
-    }
-    if (ep.ext_thr == 0) {
+      for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+    const int nk = ke - kb;
+    // prologue: NSTAGE-1 tiles in flight
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(bf2[j], af2[i], acc[i][j]);
-    }
-  }
-  const bool ext_masked = ext && ep.ext_thr != 0;
-
-  // ---- epilogue phase 1: accumulators -> LDS tile (one 8-byte write per 16x16 tile) ----
-  __syncthreads();  // staging ring is reused for the C tile
-  T* Cs = reinterpret_cast<T*>(smem);
-  constexpr int CLD = BN + 8;
-  const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = wn * WN + j * 16 + fq * 4;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (ep.bias != nullptr && n0 + col < N) {
-      if (ep.bias_f32) {
-        float4 t4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ep.bias) + n0 + col);
-        bv[0] = t4.x; bv[1] = t4.y; bv[2] = t4.z; bv[3] = t4.w;
+    for (int s = 0; s < NSTAGE - 1; ++s)
+      if (s < nk) stage(s, (kb + s) * BK);
+    for (int kt = 0; kt < nk; ++kt) {
+      // tile kt landed <=> at most (#tiles issued after kt) * PER_STAGE pieces outstanding
+      if constexpr (NSTAGE >= 3) {
+        if (kt + 1 < nk) wait_vmcnt<PER_STAGE>();
+        else wait_vmcnt<0>();
       } else {
-        load4<T>(reinterpret_cast<const T*>(ep.bias) + n0 + col, bv);
+        wait_vmcnt<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // everyone's pieces of kt landed; everyone done reading kt-1
+      asm volatile("" ::: "memory");  // no LDS access may move above the barrier
+      if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, (kb + kt + NSTAGE - 1) * BK);
+      const char* As = smem + (kt % NSTAGE) * STAGE_BYTES;
+      const char* Bs = As + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int lc = kk * 4 + fq;
+        frag_t<T> af[TM], bfv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * WM + i * 16 + fr;
+          af[i] = *reinterpret_cast<const frag_t<T>*>(As + r * ROWB + ((lc ^ (r & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * WN + j * 16 + fr;
+          bfv[j] = *reinterpret_cast<const frag_t<T>*>(Bs + r * ROWB + ((lc ^ (r & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(bfv[j], af[i], acc[i][j]);
       }
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = wm * WM + i * 16 + fr;
-      float z[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) z[e] = acc[i][j][e] * alpha + bv[e];
-      if (ext_masked) {
-        float4_ xt = mfma16<T>(bf2[j], af2[i], float4_{0.f, 0.f, 0.f, 0.f});
-        bool kp[4];
-        mift_keep4(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col, ep.ext_thr, kp);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) z[e] += kp[e] ? xt[e] * ep.ext_inv_keep : 0.f;
-      }
-      store4<T>(Cs + row * CLD + col, z);
-    }
-  }
-  __syncthreads();
+  };
 
-  // ---- epilogue phase 2: 8 columns per thread, 16-B vector I/O, whole rows ----
-  constexpr int VPR = BN / 8;
-  for (int v = tid; v < BM * VPR; v += NT) {
-    const int row = v / VPR, c8 = (v % VPR) * 8;
-    const int gr = m0 + row, gc = n0 + c8;
-    if (gr >= M || gc >= N) continue;
-    float z[8];
-    load8<T>(Cs + row * CLD + c8, z);
-    const size_t off = (size_t)gr * ldc + gc;
-    const bool full = gc + 8 <= N;
-    if (ep.pre_add != nullptr) {
-      float pa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (full) load8<T>(reinterpret_cast<const T*>(ep.pre_add) + off, pa);
-      else for (int e = 0; e < N - gc; ++e) pa[e] = (float)reinterpret_cast<const T*>(ep.pre_add)[off + e];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) z[e] += pa[e];
-    }
-    if (ep.preact != nullptr) {
-      if (full) store8<T>(reinterpret_cast<T*>(ep.preact) + off, z);
-      else for (int e = 0; e < N - gc; ++e) reinterpret_cast<T*>(ep.preact)[off + e] = (T)z[e];
-    }
-    if (ep.act != ACT_NONE) {
-      float ax[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (ep.aux != nullptr) {
-        if (full) load8<T>(reinterpret_cast<const T*>(ep.aux) + off, ax);
-        else for (int e = 0; e < N - gc; ++e) ax[e] = (float)reinterpret_cast<const T*>(ep.aux)[off + e];
+  // fused epilogue of the (m0, n0) tile from acc (+ LoRA K-extension)
+  auto epilogue = [&]() {
+    // ---- LoRA K-extension: one extra K=32 step from global (A2[M,32], B2[N,32]) ----
+    frag_t<T> af2[TM], bf2[TN];
+    const bool ext = A2 != nullptr;
+    if (ext) {
+  #pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = min(m0 + wm * WM + i * 16 + fr, M - 1);
+        af2[i] = *reinterpret_cast<const frag_t<T>*>(A2 + (size_t)r * 32 + fq * 8);
       }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) z[e] = apply_act(ep.act, z[e], ax[e]);
+  #pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = min(n0 + wn * WN + j * 16 + fr, N - 1);
+        bf2[j] = *reinterpret_cast<const frag_t<T>*>(B2 + (size_t)r * 32 + fq * 8);
+      }
+      if (ep.ext_thr == 0) {
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(bf2[j], af2[i], acc[i][j]);
+      }
     }
-    if (ep.thr != 0) {
-      bool kp[8];
-      mift_keep8(ep.seed, (uint64_t)gr * N + gc, ep.thr, kp);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) z[e] = kp[e] ? z[e] * ep.inv_keep : 0.f;
+    const bool ext_masked = ext && ep.ext_thr != 0;
+
+    // ---- epilogue phase 1: accumulators -> LDS tile (one 8-byte write per 16x16 tile) ----
+    __syncthreads();  // staging ring is reused for the C tile
+    T* Cs = reinterpret_cast<T*>(smem);
+    constexpr int CLD = BN + 8;
+    const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
+  #pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WN + j * 16 + fq * 4;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (ep.bias != nullptr && n0 + col < N) {
+        if (ep.bias_f32) {
+          float4 t4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ep.bias) + n0 + col);
+          bv[0] = t4.x; bv[1] = t4.y; bv[2] = t4.z; bv[3] = t4.w;
+        } else {
+          load4<T>(reinterpret_cast<const T*>(ep.bias) + n0 + col, bv);
+        }
+      }
+  #pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + fr;
+        float z[4];
+  #pragma unroll
+        for (int e = 0; e < 4; ++e) z[e] = acc[i][j][e] * alpha + bv[e];
+        if (ext_masked) {
+          float4_ xt = mfma16<T>(bf2[j], af2[i], float4_{0.f, 0.f, 0.f, 0.f});
+          bool kp[4];
+          mift_keep4(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col, ep.ext_thr, kp);
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) z[e] += kp[e] ? xt[e] * ep.ext_inv_keep : 0.f;
+        }
+        store4<T>(Cs + row * CLD + col, z);
+      }
     }
-    if (ep.residual != nullptr) {
-      float rv[8];
-      if (full) load8<T>(reinterpret_cast<const T*>(ep.residual) + off, rv);
-      else for (int e = 0; e < N - gc; ++e) rv[e] = (float)reinterpret_cast<const T*>(ep.residual)[off + e];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) z[e] += rv[e];
+    __syncthreads();
+
+    // ---- epilogue phase 2: 8 columns per thread, 16-B vector I/O, whole rows ----
+    constexpr int VPR = BN / 8;
+    for (int v = tid; v < BM * VPR; v += NT) {
+      const int row = v / VPR, c8 = (v % VPR) * 8;
+      const int gr = m0 + row, gc = n0 + c8;
+      if (gr >= M || gc >= N) continue;
+      float z[8];
+      load8<T>(Cs + row * CLD + c8, z);
+      const size_t off = (size_t)gr * ldc + gc;
+      const bool full = gc + 8 <= N;
+      if (ep.pre_add != nullptr) {
+        float pa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (full) load8<T>(reinterpret_cast<const T*>(ep.pre_add) + off, pa);
+        else for (int e = 0; e < N - gc; ++e) pa[e] = (float)reinterpret_cast<const T*>(ep.pre_add)[off + e];
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] += pa[e];
+      }
+      if (ep.preact != nullptr) {
+        if (full) store8<T>(reinterpret_cast<T*>(ep.preact) + off, z);
+        else for (int e = 0; e < N - gc; ++e) reinterpret_cast<T*>(ep.preact)[off + e] = (T)z[e];
+      }
+      if (ep.act != ACT_NONE) {
+        float ax[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ep.aux != nullptr) {
+          if (full) load8<T>(reinterpret_cast<const T*>(ep.aux) + off, ax);
+          else for (int e = 0; e < N - gc; ++e) ax[e] = (float)reinterpret_cast<const T*>(ep.aux)[off + e];
+        }
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = apply_act(ep.act, z[e], ax[e]);
+      }
+      if (ep.thr != 0) {
+        bool kp[8];
+        mift_keep8(ep.seed, (uint64_t)gr * N + gc, ep.thr, kp);
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = kp[e] ? z[e] * ep.inv_keep : 0.f;
+      }
+      if (ep.residual != nullptr) {
+        float rv[8];
+        if (full) load8<T>(reinterpret_cast<const T*>(ep.residual) + off, rv);
+        else for (int e = 0; e < N - gc; ++e) rv[e] = (float)reinterpret_cast<const T*>(ep.residual)[off + e];
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] += rv[e];
+      }
+      if (full) store8<T>(C + off, z);
+      else for (int e = 0; e < N - gc; ++e) C[off + e] = (T)z[e];
     }
-    if (full) store8<T>(C + off, z);
-    else for (int e = 0; e < N - gc; ++e) C[off + e] = (T)z[e];
-  }
+  };
+
+  const int nk_all = K / BK;
+  if constexpr (!SKM) {
+    // ---- data-parallel tile, XCD-aware bijective block remap (T1) ----
+    const int nblk = gridDim.x;  // tiles [0, gridDim.x) (all of them unless stream-K takes the tail)
+    int bid = blockIdx.x;
+    {
+      const int q = nblk / 8, r = nblk % 8;
+      const int xcd = bid % 8, loc = bid / 8;
+      bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    }
+    m0 = (bid / ntn) * BM;
+    n0 = (bid % ntn) * BN;
+    mainloop(0, nk_all);
+    epilogue();
+    return;
+  } else {
+    // ---- split-K tail (separate instantiation: its bookkeeping must not cost the DP kernel
+    // registers).  Block b handles k-chunk (b % S) of tile tile0 + b / S; the block holding a
+    // tile's LAST chunk finishes it after the lower-index chunk blocks (dispatched before it,
+    // running concurrently: no cycles, next to no waiting) released their fp32 partials.
+    const int S = sk.gx;
+    const int tl = blockIdx.x / S, cidx = blockIdx.x % S;
+    const int tile = sk.tile0 + tl;
+    m0 = (tile / ntn) * BM;
+    n0 = (tile % ntn) * BN;
+    mainloop((int)((long)cidx * nk_all / S), (int)((long)(cidx + 1) * nk_all / S));
+    constexpr int SLOT = TM * TN * NT;  // float4 per partial tile
+    if (cidx < S - 1) {
+      float4_* dst = reinterpret_cast<float4_*>(sk.ws) + (size_t)blockIdx.x * SLOT;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) dst[(i * TN + j) * NT + tid] = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(sk.flags + tl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      while (__hip_atomic_load(sk.flags + tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1)
+        __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(sk.flags + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    for (int c = 1; c < S; ++c) {
+      const float4_* src = reinterpret_cast<const float4_*>(sk.ws) + (size_t)(blockIdx.x - c) * SLOT;
+      // in groups of 4 float4: keeps the scheduler from hoisting all TM*TN loads at once
+      // (a second accumulator-sized register set -> spills on the 256x256 tile)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] += src[(i * TN + j) * NT + tid];
+          if (((i * TN + j) & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    epilogue();
+  }  // SKM
+}
+
+int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+// persistent, self-re-arming stream-K tile counters (zeroed once; finishers reset theirs)
+int* sk_flags(int n) {
+  static at::Tensor flags;
+  if (!flags.defined() || flags.numel() < n)
+    flags = at::zeros({std::max<int64_t>(n, 1 << 16)}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA));
+  return flags.data_ptr<int>();
+}
+
+int sk_mode_env() {
+  static int v = [] { const char* e = getenv("MIFT_GEMM_SK"); return e ? atoi(e) : -1; }();
+  return v;  // -1 auto, 0 off, 1 force
 }
 
 template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE>
@@ -321,16 +415,57 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
   constexpr int EPI_BYTES = BM * (BN + 8) * 2;
   constexpr int RING = NSTAGE * STAGE_BYTES;
   constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
+  constexpr int NT = NWM * NWN * 64;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   const int nblk = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  auto kern = gemm_nt_kernel<T, BM, BN, NWM, NWN, NSTAGE>;
+  // the 256x256 tile has no register headroom for the split-K fixup (it would spill): DP only
+  constexpr bool HAS_SK = BM * BN <= 256 * 128;
+  auto kern = gemm_nt_kernel<T, BM, BN, NWM, NWN, NSTAGE, false>;
+  auto kern_sk = gemm_nt_kernel<T, BM, BN, NWM, NWN, NSTAGE, HAS_SK>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)kern_sk, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(nblk), dim3(NWM * NWN * 64), SMEM, st, (const T*)a.data_ptr(), (const T*)b.data_ptr(),
-                     (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), ep);
+  // hybrid data-parallel + split-K tail: full waves of tiles run data-parallel; a ragged last
+  // wave of rem tiles (< ~85 % of the resident slots) is split S ways along K so it fills the
+  // chip: time ~ ceil(rem*S/G)/S tile-times instead of 1 (S chosen on that model + fixup cost)
+  constexpr int BPC = (160 * 1024 / SMEM) < (2048 / NT) ? (160 * 1024 / SMEM) : (2048 / NT);
+  const int G = num_cus() * (BPC > 0 ? BPC : 1);
+  const int nk = K / BK;
+  const int rem = nblk % G;
+  int sk_tiles = 0, S = 1;
+  const int mode = sk_mode_env();
+  if (HAS_SK && mode != 0 && rem != 0 && (mode == 1 || rem * 100 < G * 85)) {
+    double best = 1.0;
+    // chunks of >= 16 k-tiles: below that the fp32 partial round trip costs more than the
+    // balanced wave saves (measured: K=768 GEMMs lost 2-4x with 3-k-tile chunks)
+    for (int s = 2; s <= 8 && nk / s >= 16; ++s) {
+      const double cost = (double)((rem * s + G - 1) / G) / s + 0.03 * (s - 1);
+      if (cost < best - 1e-9) { best = cost; S = s; }
+    }
+    if (S > 1) sk_tiles = rem;
+  }
+  const int dp_tiles = nblk - sk_tiles;
+  SkArgs sk{};
+  const T* A = (const T*)a.data_ptr();
+  const T* Bp = (const T*)b.data_ptr();
+  T* Cp = (T*)c.data_ptr();
+  if (dp_tiles > 0)
+    hipLaunchKernelGGL(kern, dim3(dp_tiles), dim3(NT), SMEM, st, A, Bp, Cp, a2, b2, M, N, K, (int)a.stride(0),
+                       (int)b.stride(0), (int)c.stride(0), ep, sk);
+  if (sk_tiles > 0) {
+    auto ws = at::empty({(int64_t)sk_tiles * S * BM * BN}, a.options().dtype(at::kFloat));
+    sk.enabled = 1;
+    sk.tile0 = dp_tiles;
+    sk.ntiles = sk_tiles;
+    sk.gx = S;
+    sk.ws = ws.data_ptr<float>();
+    sk.flags = sk_flags(sk_tiles);
+    hipLaunchKernelGGL(kern_sk, dim3(sk_tiles * S), dim3(NT), SMEM, st, A, Bp, Cp, a2, b2, M, N, K, (int)a.stride(0),
+                       (int)b.stride(0), (int)c.stride(0), ep, sk);
+  }
 }
 
 // Tile configurations (tile id -> geometry):
@@ -344,13 +479,16 @@ template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
   if (tile == 0) {
-    // auto (measured on MI355X, tools/bench_kernels.py -> profiles/): the
-    // 256x128 3-stage ring wins on long-K, wide-N problems (OPT-2.7B qkv/fc1:
-    // +12-15%); the 128x128 tile wins everywhere else (distilgpt2 shapes:
-    // K = 768..3072) because its shorter prologue/epilogue dominates.
-    const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128);
+    // auto, from tools/bench_kernels.py on MI355X (profiles/bench_gemm_tiles_sk.json):
+    //  * 256x256 (tile 5) wins whenever there are enough big tiles and K is not tiny
+    //    (OPT-2.7B qkv/out/fc1 fwd, fc2 dgrad, LM heads: +5..30 % over 128x128);
+    //  * long-K problems with few 256x256 tiles (N = 2560, K >= 4096: fc2 fwd, qkv/fc1 dgrad)
+    //    run 128x256 + the split-K ragged-wave tail (+15..30 %);
+    //  * distilgpt2-scale problems (K = 768..3072, N <= 3072) keep the 128x128 tile.
+    const long n256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-    if (K >= 2048 && N >= 2048 && t256 >= 384) tile = 1;
+    if (K >= 4096 && n256 < 256 && t128 >= 128) tile = 6;
+    else if ((K >= 1024 && n256 >= 128) || n256 >= 2048) tile = 5;
     else if (t128 >= 64) tile = 3;
     else tile = 4;
   }

@@ -60,17 +60,16 @@ MIFT_HD frag_t<T> masked_frag(const T* p, uint64_t seed, uint64_t idx0, uint32_t
 // ------------------------------------------------------------------ lora_proj
 // Grid = (M/32 row blocks) x KS K-splits: with only M/32 row blocks (128 for
 // M = 4096) the kernel filled half of the 256 CUs and ran latency-bound; the
-// K-splits give >= ~1024 blocks.  KS > 1: every block adds its [32,32] fp32
-// partial into the zeroed workspace ``ws`` with atomics, and the LAST block of
-// a row block (per-row-block arrival counter after a release fence) converts
-// the finished sums to 16-bit — one launch, no second pass.
+// K-splits give ~1024 blocks.  KS > 1: every block stores its [32,32] fp32
+// partial to ws[kss] with plain stores and lora_proj_reduce sums the KS
+// partials into the 16-bit output (an in-kernel last-block reduction needs a
+// device-scope fence per block, ~3.5 us on gfx950 — slower than a launch).
 template <typename T>
 __global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X, const T* __restrict__ W,
                                                         T* __restrict__ out, int M, int K, int ldx, float alpha,
                                                         uint64_t seed, uint32_t thr, float inv_keep, int KS,
-                                                        float* __restrict__ ws, int* __restrict__ cnt) {
+                                                        float* __restrict__ ws) {
   __shared__ float red[4][32][33];
-  __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, fr = lane & 15;
   const int mb = blockIdx.x / KS, kss = blockIdx.x % KS;
@@ -146,23 +145,30 @@ __global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X,
     }
     return;
   }
+  float* wp = ws + (int64_t)kss * M * 32;
   for (int e = tid; e < 32 * 32; e += 256) {
     const int r = e >> 5, c = e & 31;
-    if (m0 + r < M) atomicAdd(ws + (int64_t)(m0 + r) * 32 + c, red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c]);
+    if (m0 + r < M) wp[(int64_t)(m0 + r) * 32 + c] = red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c];
   }
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) last = atomicAdd(cnt + mb, 1) == KS - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  for (int e = tid; e < 32 * 32; e += 256) {
-    const int r = e >> 5, c = e & 31;
-    if (m0 + r < M) {
-      const float v = __hip_atomic_load(ws + (int64_t)(m0 + r) * 32 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      out[(int64_t)(m0 + r) * 32 + c] = (T)(v * alpha);
-    }
+}
+
+// out[m, c] = alpha * sum_s ws[s, m, c]  (8 outputs per thread, 16-B stores)
+template <typename T>
+__global__ __launch_bounds__(256) void lora_proj_reduce(const float* __restrict__ ws, T* __restrict__ out, int M,
+                                                         int KS, float alpha) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  const int64_t n = (int64_t)M * 32;
+  if (i >= n) return;
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int s = 0; s < KS; ++s) {
+    const float4 a = *reinterpret_cast<const float4*>(ws + s * n + i);
+    const float4 b = *reinterpret_cast<const float4*>(ws + s * n + i + 4);
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+    v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
   }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= alpha;
+  store8<T>(out + i, v);
 }
 
 // ----------------------------------------------------------------- lora_wgrad
@@ -302,24 +308,33 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   const float ik = p > 0 ? mift_inv_keep(p) : 1.f;
   const int mblocks = (M + 31) / 32, nks = K / 32;
   // K-splits so the launch covers the chip (>= ~1024 blocks), >= 4 k-steps (one per wave) each
-  const int KS = std::max(1, std::min(std::max(1, nks / 4), (1024 + mblocks - 1) / mblocks));
+  static const int ks_env = [] { const char* e = getenv("MIFT_LORA_KS"); return e ? atoi(e) : 0; }();
+  // split K only when the row blocks alone leave CUs idle (measured: distilgpt2, M = 8192 ->
+  // 256 row blocks, is 3 % faster unsplit; OPT micro-batches of M = 4096 gain 2 % from KS = 8)
+  int KS = mblocks >= 192 ? 1 : std::max(1, std::min(std::max(1, nks / 4), (1024 + mblocks - 1) / mblocks));
+  if (ks_env > 0) KS = std::max(1, std::min(ks_env, std::max(1, nks / 4)));  // A/B override
   float* ws = nullptr;
-  int* cnt = nullptr;
   at::Tensor wsb;
   if (KS > 1) {
-    wsb = at::zeros({(int64_t)M * 32 + mblocks}, x.options().dtype(at::kFloat));
+    wsb = at::empty({(int64_t)KS * M * 32}, x.options().dtype(at::kFloat));
     ws = wsb.data_ptr<float>();
-    cnt = reinterpret_cast<int*>(ws + (int64_t)M * 32);
   }
   const int grid = mblocks * KS;
   if (x.scalar_type() == at::kBFloat16)
     lora_proj_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)x.data_ptr(), (const bf16*)w.data_ptr(),
                                                  (bf16*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                 (uint64_t)seed, thr, ik, KS, ws, cnt);
+                                                 (uint64_t)seed, thr, ik, KS, ws);
   else
     lora_proj_kernel<fp16><<<grid, 256, 0, st>>>((const fp16*)x.data_ptr(), (const fp16*)w.data_ptr(),
                                                  (fp16*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                 (uint64_t)seed, thr, ik, KS, ws, cnt);
+                                                 (uint64_t)seed, thr, ik, KS, ws);
+  if (KS > 1) {
+    const int rg = (int)(((int64_t)M * 32 / 8 + 255) / 256);
+    if (x.scalar_type() == at::kBFloat16)
+      lora_proj_reduce<bf16><<<rg, 256, 0, st>>>(ws, (bf16*)out.data_ptr(), M, KS, (float)alpha);
+    else
+      lora_proj_reduce<fp16><<<rg, 256, 0, st>>>(ws, (fp16*)out.data_ptr(), M, KS, (float)alpha);
+  }
   return out;
 }
 
