@@ -1,0 +1,48 @@
+"""Flash-attention kernel timings (fwd, bwd) at the model shapes, vs torch SDPA.
+
+  python tools/bench_attn.py [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import mift  # noqa: E402
+from tools.bench_kernels import timeit  # noqa: E402
+
+SHAPES = [("distilgpt2", 32, 256, 12, 64, torch.bfloat16, 0.1), ("opt-2.7b", 8, 512, 32, 80, torch.float16, 0.0),
+          ("opt-6.7b", 4, 1024, 32, 128, torch.float16, 0.0)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    C = mift._ext.require()
+    rows = []
+    for name, B, S, H, hd, dt, p in SHAPES:
+        qkv = torch.randn(B * S, 3 * H * hd, device="cuda", dtype=dt)
+        sc = hd ** -0.5
+        o, lse = C.attn_fwd(qkv, B, S, H, hd, sc, p, 1, None)
+        do = torch.randn_like(o)
+        tf = timeit(lambda: C.attn_fwd(qkv, B, S, H, hd, sc, p, 1, None))
+        tb = timeit(lambda: C.attn_bwd(do, qkv, o, lse, B, S, H, hd, sc, p, 1, None))
+        q, k, v = qkv.view(B, S, 3, H, hd).permute(2, 0, 3, 1, 4)
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        ts = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True))
+        fl = 4.0 * B * H * S * S * hd / 2  # causal fwd flops
+        row = {"name": name, "B": B, "S": S, "H": H, "hd": hd, "fwd_ms": round(tf, 4), "fwd_tflops": round(fl / tf / 1e9, 1),
+               "bwd_ms": round(tb, 4), "bwd_tflops": round(2.5 * fl / tb / 1e9, 1), "sdpa_fwd_ms": round(ts, 4)}
+        print(json.dumps(row), flush=True)
+        rows.append(row)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -35,6 +35,7 @@ def timeit(fn, iters=20, rounds=5):
     return statistics.median(ts)
 
 
+TILES = [int(t) for t in os.environ.get("TILES", "0,1,2,3,4,5,6").split(",")]
 GEMM_SHAPES = [
     # (name, M, N, K)  distilgpt2, 32x256 tokens per rank
     ("c_attn.fwd", 8192, 2304, 768),
@@ -63,7 +64,7 @@ def bench_gemm(results, shapes=None, dtype=torch.bfloat16):
         b = torch.randn(N, K, device="cuda", dtype=dtype)
         fl = 2.0 * M * N * K
         row = {"name": name, "M": M, "N": N, "K": K}
-        for tile in (0, 1, 2, 3, 4, 5, 6):
+        for tile in TILES:
             t = timeit(lambda: C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, tile, None, None, 0.0, 0))
             row[f"mift_t{tile}_ms"] = round(t, 4)
             row[f"mift_t{tile}_tflops"] = round(fl / t / 1e9, 1)

@@ -114,7 +114,8 @@ class HashWordTokenizer:
 
     def _ids(self, text):
         import zlib
-        return [1000 + zlib.crc32(w.encode()) % (self.vocab_size - 1000) for w in re.findall(r"\w+", text.lower())]
+        base = min(1000, self.vocab_size // 2)  # above the special ids; small test vocabs too
+        return [base + zlib.crc32(w.encode()) % (self.vocab_size - base) for w in re.findall(r"\w+", text.lower())]
 
     def __call__(self, texts, max_length=128, **_):
         ids = np.zeros((len(texts), max_length), dtype=np.int64)

@@ -61,3 +61,12 @@ def save_hf_config(model, d):
     os.makedirs(d, exist_ok=True)
     with open(os.path.join(d, "config.json"), "w") as f:
         json.dump(model.config.to_hf_dict(), f, indent=2)
+
+
+def save_hf_model(model, d):
+    """HF-layout checkpoint dir: ``model.safetensors`` (all weights) + ``config.json``."""
+    from safetensors.torch import save_file
+    os.makedirs(d, exist_ok=True)
+    save_file({k: v.detach().contiguous().cpu() for k, v in model.state_dict().items()},
+              os.path.join(d, "model.safetensors"), metadata={"format": "pt"})
+    save_hf_config(model, d)
