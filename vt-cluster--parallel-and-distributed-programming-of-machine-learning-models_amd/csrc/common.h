@@ -45,13 +45,31 @@ MIFT_HD uint32_t mift_hash_pair(uint64_t seed, uint64_t pair) {
   const uint32_t lo = (uint32_t)pair, hi = (uint32_t)(pair >> 32);
   return mix32((lo * 0x9E3779B9U) ^ mix32(hi ^ (uint32_t)(seed >> 32)) ^ (uint32_t)seed);
 }
+// Hoisted form of mift_hash_pair: hm = mix32(hi ^ seed_hi) depends only on the
+// pair's high word, which is 0 for every tensor below 2^33 elements -> a kernel
+// computes it once (mift_hmix(seed, 0)) and pays 3 instead of 5 multiplies per
+// pair.  Bit-identical to mift_hash_pair for pairs with that high word.
+MIFT_HD uint32_t mift_hmix(uint64_t seed, uint32_t hi) { return mix32(hi ^ (uint32_t)(seed >> 32)); }
+MIFT_HD uint32_t mift_hash_lo(uint64_t seed, uint32_t hm, uint32_t lo) {
+  return mix32((lo * 0x9E3779B9U) ^ hm ^ (uint32_t)seed);
+}
 MIFT_HD uint32_t mift_bits16(uint64_t seed, uint64_t idx) {
   return (mift_hash_pair(seed, idx >> 1) >> ((idx & 1) << 4)) & 0xFFFFu;
 }
 MIFT_HD bool mift_keep(uint64_t seed, uint64_t idx, uint32_t thr) { return mift_bits16(seed, idx) >= thr; }
 // 8 consecutive elements: 4 hashes when idx0 is even (the common case).
 MIFT_HD void mift_keep8(uint64_t seed, uint64_t idx0, uint32_t thr, bool* k) {
-  if ((idx0 & 1) == 0) {
+  const uint32_t lo0 = (uint32_t)(idx0 >> 1);
+  if ((idx0 & 1) == 0 && lo0 <= 0xFFFFFFFCu) {
+    // the 4 pairs share their high word: one hoisted mix (14 instead of 20 multiplies)
+    const uint32_t hm = mift_hmix(seed, (uint32_t)(idx0 >> 33));
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const uint32_t h = mift_hash_lo(seed, hm, lo0 + (e >> 1));
+      k[e] = (h & 0xFFFFu) >= thr;
+      k[e + 1] = (h >> 16) >= thr;
+    }
+  } else if ((idx0 & 1) == 0) {
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {
       const uint32_t h = mift_hash_pair(seed, (idx0 + e) >> 1);
@@ -196,6 +214,16 @@ MIFT_HD void store4(T* p, const float* in) {
     *reinterpret_cast<short4_*>(p) = v;
   }
 }
+// keep bits of idx0..idx0+3 (idx0 even, all pairs with high word matching hm)
+MIFT_HD void mift_keep4_hm(uint64_t seed, uint32_t hm, uint64_t idx0, uint32_t thr, bool* k) {
+  const uint32_t lo = (uint32_t)(idx0 >> 1);
+  const uint32_t h0 = mift_hash_lo(seed, hm, lo), h1 = mift_hash_lo(seed, hm, lo + 1);
+  k[0] = (h0 & 0xFFFFu) >= thr; k[1] = (h0 >> 16) >= thr;
+  k[2] = (h1 & 0xFFFFu) >= thr; k[3] = (h1 >> 16) >= thr;
+}
+// bare v_exp_f32 (no denormal range handling; softmax inputs are <= 0 or -inf)
+MIFT_HD float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 MIFT_HD void mift_keep4(uint64_t seed, uint64_t idx0, uint32_t thr, bool* k) {
   if ((idx0 & 1) == 0) {
     const uint32_t h0 = mift_hash_pair(seed, idx0 >> 1), h1 = mift_hash_pair(seed, (idx0 >> 1) + 1);

@@ -171,6 +171,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
   const int q0 = qt * BQ + wave * 16;
   const int myq = q0 + qc;
   const float c2 = scale * LOG2E;
+  const bool hz = (uint64_t)B * H * S * S < (1ull << 33);  // dropout pairs' high word is 0: hoisted hash
+  const uint32_t hm0 = mift_hmix(seed, 0);
 
   vec8<T> qf[G::NKS];
   load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
@@ -222,29 +224,42 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(m, tmax);
-    const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - mnew);
-    m = mnew;
+    // lazy rescale: the running max only moves when some row's tile max exceeds it by
+    // > 2^8 (p <= 256 stays exact in fp32 and representable in bf16/fp16), so most tiles
+    // skip the O rescale and its accumulator round trips (wave-uniform branch)
+    const bool resc = __any(tmax > m + 8.f);
+    float alpha = 1.f;
+    if (resc) {
+      const float mnew = fmaxf(m, tmax);
+      alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mnew);
+      m = mnew;
+    }
     float psum = 0.f;
     vec8<T> pf[2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       bool kp[4] = {true, true, true, true};
-      if (thr != 0) mift_keep4(seed, ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4, thr, kp);
+      if (thr != 0) {
+        const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
+        if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
+        else mift_keep4(seed, i0, thr, kp);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float p = (mnew == -INFINITY) ? 0.f : exp2f(st[t][r] - mnew);
+        float p = (m == -INFINITY) ? 0.f : fast_exp2(st[t][r] - m);
         psum += p;
         if (thr != 0) p = kp[r] ? p * inv_keep : 0.f;
         pf[t >> 1][(t & 1) * 4 + r] = (T)p;
       }
     }
     l = l * alpha + psum;
+    if (resc) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float ar = __shfl(alpha, g * 4 + r, 64);
+      for (int r = 0; r < 4; ++r) {
+        const float ar = __shfl(alpha, g * 4 + r, 64);
 #pragma unroll
-      for (int i = 0; i < G::NOT; ++i) o[i][r] *= ar;
+        for (int i = 0; i < G::NOT; ++i) o[i][r] *= ar;
+      }
     }
 #pragma unroll
     for (int i = 0; i < G::NOT; ++i)
@@ -349,11 +364,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
         pa = mfma16(ld_frag<T>(Vs + (t * 16 + qc) * G::RS + (4 * s + g) * 16), df[s], pa);
       }
       bool kp[4] = {true, true, true, true};
-      if (thr != 0) mift_keep4(seed, ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4, thr, kp);
+      if (thr != 0) {
+        const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
+        if ((uint64_t)B * H * S * S < (1ull << 33) && !(i0 & 1)) mift_keep4_hm(seed, mift_hmix(seed, 0), i0, thr, kp);
+        else mift_keep4(seed, i0, thr, kp);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + t * 16 + g * 4 + r;
-        const float p = (key > myq || key >= klen) ? 0.f : exp2f(sa[r] * c2 - lse2);
+        const float p = (key > myq || key >= klen) ? 0.f : fast_exp2(sa[r] * c2 - lse2);
         float dp = pa[r];
         if (thr != 0) dp = kp[r] ? dp * inv_keep : 0.f;
         dsf[t >> 1][(t & 1) * 4 + r] = (T)(p * (dp - Dq));
@@ -462,7 +481,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const T* __restrict_
         const int qa = min(qb + t * 16 + g * 4 + 2 * odd, S - 1);
         const uint64_t p0 = (((uint64_t)bh * S + qa) * S + mykey) >> 1;
         const uint64_t p1 = (((uint64_t)bh * S + min(qa + 1, S - 1)) * S + mykey) >> 1;
-        const uint32_t h0 = mift_hash_pair(seed, p0), h1 = mift_hash_pair(seed, p1);
+        uint32_t h0, h1;
+        if ((uint64_t)B * H * S * S < (1ull << 33)) {  // high words 0: hoisted hash (bit-identical)
+          const uint32_t hm = mift_hmix(seed, 0);
+          h0 = mift_hash_lo(seed, hm, (uint32_t)p0);
+          h1 = mift_hash_lo(seed, hm, (uint32_t)p1);
+        } else {
+          h0 = mift_hash_pair(seed, p0);
+          h1 = mift_hash_pair(seed, p1);
+        }
         const uint32_t o0 = __shfl_xor(h0, 1, 64), o1 = __shfl_xor(h1, 1, 64);
         hb[0] = odd ? o0 : h0;
         hb[1] = odd ? o1 : h1;
@@ -474,7 +501,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const T* __restrict_
         const int ql = t * 16 + g * 4 + r;
         const int q = qb + ql;
         const bool valid = q < S && mykey <= q && mykey < klen;
-        const float p = valid ? exp2f(sa[r] * c2 - lse_s[ql]) : 0.f;
+        const float p = valid ? fast_exp2(sa[r] * c2 - lse_s[ql]) : 0.f;
         float pd = p, dp = pa[r];
         if (thr != 0) {
           const uint32_t bits = (S & 1) ? mift_bits16(seed, ((uint64_t)bh * S + q) * S + mykey)
