@@ -35,7 +35,7 @@ def timeit(fn, iters=20, rounds=5):
     return statistics.median(ts)
 
 
-TILES = [int(t) for t in os.environ.get("TILES", "0,1,2,3,4,5,6").split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "0,1,2,3,4,5,6,7").split(",")]
 GEMM_SHAPES = [
     # (name, M, N, K)  distilgpt2, 32x256 tokens per rank
     ("c_attn.fwd", 8192, 2304, 768),

@@ -475,6 +475,8 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
 //   4: 64x64,   4 waves (2x2), 3-stage ring (48 KiB)               — tiny problems
 //   5: 256x256, 8 waves (2x4), 2-stage ring (128 KiB; C tile 132 KiB) — halves L2->CU bytes/MAC vs 128x128
 //   6: 128x256, 8 waves (2x4), 2-stage ring (96 KiB)
+//   7: 128x96,  4 waves (2x2, wave tile 64x48), 2-stage ring (56 KiB, 2 blocks/CU) — balances
+//      ragged waves: N=768 gives 512 tiles = exactly one wave of 2x256 slots (128x128: 384)
 template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
@@ -489,8 +491,16 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
     if (K >= 4096 && n256 < 256 && t128 >= 128) tile = 6;
     else if ((K >= 1024 && n256 >= 128) || n256 >= 2048) tile = 5;
-    else if (t128 >= 64) tile = 3;
-    else tile = 4;
+    else if (t128 >= 64) {
+      tile = 3;
+      // 128x96 when its whole-wave count x tile area beats 128x128's (5 % per-tile
+      // efficiency handicap for the smaller tile)
+      if (N % 96 == 0) {
+        const long G = 2L * num_cus();
+        const long t96 = (long)((M + 127) / 128) * (N / 96);
+        if ((t96 + G - 1) / G * 3 * 105 < (t128 + G - 1) / G * 4 * 100) tile = 7;
+      }
+    } else tile = 4;
   }
   switch (tile) {
     case 1: launch_gemm<T, 256, 128, 4, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
@@ -498,6 +508,7 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     case 3: launch_gemm<T, 128, 128, 2, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 5: launch_gemm<T, 256, 256, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 6: launch_gemm<T, 128, 256, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 7: launch_gemm<T, 128, 96, 2, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     default: launch_gemm<T, 64, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
   }
 }
