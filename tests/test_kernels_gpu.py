@@ -206,6 +206,32 @@ def test_lora_proj_and_wgrad(p):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("rank,D", [(8, 768), (28, 2560), (16, 1024)])
+@pytest.mark.parametrize("p", [0.0, 0.05])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_rowproj_fused_kernels(rank, D, p, dt):
+    """LN fwd + LoRA projection and dropout-bwd + dT (csrc/kernels/rowproj.hip) vs fp32 reference."""
+    C = _C()
+    torch.manual_seed(11)
+    M = 777
+    x = torch.randn(M, D, device="cuda", dtype=dt)
+    w = (1 + 0.1 * torch.randn(D, device="cuda")).to(dt)
+    b = (0.1 * torch.randn(D, device="cuda")).to(dt)
+    pw = torch.zeros(32, D, device="cuda", dtype=dt)
+    pw[:rank] = (torch.randn(rank, D, device="cuda") * 0.05).to(dt)
+    y, mean, rstd, t = C.layer_norm_fwd_proj(x, w, b, 1e-5, pw, rank, 1.5, p, 77)
+    y0, _, _ = C.layer_norm_fwd(x, w, b, 1e-5)
+    torch.testing.assert_close(y, y0, atol=0, rtol=0)
+    yd = ref.dropout(y.float(), p, 77)
+    torch.testing.assert_close(t.float(), 1.5 * yd @ pw.float().t(), atol=4e-2, rtol=3e-2)
+    gz, dt_ = C.mask_proj(x, p, 99, pw, rank, 2.0)
+    gexp = ref.dropout(x.float(), p, 99)
+    torch.testing.assert_close(gz.float(), gexp, atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(dt_.float(), 2.0 * gz.float() @ pw.float().t(), atol=5e-2, rtol=3e-2)
+    if p == 0.0:
+        assert gz.data_ptr() == x.data_ptr()
+
+
 def test_gemm_ext_masked():
     C = _C()
     torch.manual_seed(9)

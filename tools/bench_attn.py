@@ -14,7 +14,8 @@ import torch  # noqa: E402
 import mift  # noqa: E402
 from tools.bench_kernels import timeit  # noqa: E402
 
-SHAPES = [("distilgpt2", 32, 256, 12, 64, torch.bfloat16, 0.1), ("opt-2.7b", 8, 512, 32, 80, torch.float16, 0.0),
+SHAPES = [("distilgpt2", 32, 256, 12, 64, torch.bfloat16, 0.1), ("distilgpt2-p0", 32, 256, 12, 64, torch.bfloat16, 0.0),
+          ("opt-2.7b", 8, 512, 32, 80, torch.float16, 0.0),
           ("opt-6.7b", 4, 1024, 32, 128, torch.float16, 0.0)]
 
 

@@ -1,0 +1,62 @@
+"""Summarise rocprofv3 --pmc CSV runs per kernel (sum over dispatches).
+
+  python tools/pmc_summary.py <pmc_dir> [<pmc_dir> ...] [--top N]
+
+Per kernel: dispatches, mean duration, and derived ratios:
+  mfma_busy  = SQ_VALU_MFMA_BUSY_CYCLES / (dur_ns * clk_GHz * 1024 SIMDs)   (clk 2.4 GHz)
+  wait/issue = SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY as % of SQ_WAVE_CYCLES
+  lds_conf   = SQ_LDS_BANK_CONFLICT per dispatch
+  hbm_GBs    = 2 * FETCH_SIZE(KB) / dur   (gfx950 FETCH_SIZE counts half the bytes of
+               wide coalesced reads: MI355X_MICROARCH.md "FETCH_SIZE")
+"""
+import collections
+import csv
+import glob
+import os
+import sys
+
+CLK_GHZ = 2.4
+SIMDS = 256 * 4
+
+
+def load(dirs):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    durs = collections.defaultdict(dict)
+    for d in dirs:
+        for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(p)):
+                k = r["Kernel_Name"]
+                agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                durs[k][(p, r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return agg, durs
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    top = 20
+    if "--top" in sys.argv:
+        top = int(sys.argv[sys.argv.index("--top") + 1])
+        args = [a for a in args if a != str(top)]
+    agg, durs = load(args)
+    rows = []
+    for k, c in agg.items():
+        d = durs[k]
+        tot = sum(d.values())
+        rows.append((tot, k, c, len(d)))
+    rows.sort(reverse=True)
+    print(f"{'total_us':>9} {'n':>5} {'avg_us':>8} {'mfma%':>6} {'wait%':>6} {'stall%':>6} {'issue%':>6} "
+          f"{'ldsconf/disp':>12} {'hbm_GB/s':>9}  kernel")
+    for tot, k, c, n in rows[:top]:
+        # counters were collected in separate passes: scale each by its own pass's dispatches
+        avg = tot / n
+        wc = c.get("SQ_WAVE_CYCLES", 0.0)
+        f = lambda name: (100.0 * c[name] / wc) if wc and name in c else float("nan")
+        mfma = 100.0 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (tot * CLK_GHZ * SIMDS) * 2 if "SQ_VALU_MFMA_BUSY_CYCLES" in c else float("nan")
+        hbm = (2 * c["FETCH_SIZE"] * 1024 / (tot * 1e-9) / 1e9) / 2 if "FETCH_SIZE" in c else float("nan")
+        lds = c.get("SQ_LDS_BANK_CONFLICT", float("nan")) / (n / 2)
+        print(f"{tot/1e3:9.1f} {n:5d} {avg/1e3:8.1f} {mfma:6.1f} {f('SQ_WAIT_ANY'):6.1f} {f('SQ_WAIT_INST_ANY'):6.1f} "
+              f"{f('SQ_ACTIVE_INST_ANY'):6.1f} {lds:12.0f} {hbm:9.0f}  {k[:90]}")
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,21 @@
 
 #define MIFT_HD __device__ __forceinline__
 
+// Graph-replayable dropout seeds.  mift.models.layers.seed_for(base, step, site) =
+// fin(base*C1 + step*C2 + site*C3) with fin(x) = (x ^ x>>31) & (2^63-1).  Eager launches pass
+// the finished seed and sstep == nullptr.  Under hipGraph capture (mift.train.graph) the host
+// passes pre = base*C1 + site*C3 and sstep -> a device int64 micro-step counter, so every
+// replay of the same captured kernels draws the masks of a new micro-step, bit-identical to
+// the eager path.  Kernels take `seed, sstep` and call mift_seed once at entry.
+__device__ __forceinline__ uint64_t mift_seed(uint64_t s, const int64_t* sstep) {
+  if (sstep == nullptr) return s;
+  uint64_t x = s + (uint64_t)(*sstep) * 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 31;
+  return x & 0x7FFFFFFFFFFFFFFFull;
+}
+// host: the device micro-step counter bound by mift._C.set_seed_step (nullptr = eager)
+const int64_t* mift_seed_step();
+
 typedef __bf16 bf16;
 typedef _Float16 fp16;
 

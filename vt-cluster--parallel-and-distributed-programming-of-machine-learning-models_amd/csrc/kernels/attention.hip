@@ -151,7 +151,8 @@ template <typename T, int HD>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ kv_len,
                                                        int B, int S, int H, float scale, uint64_t seed,
-                                                       uint32_t thr, float inv_keep) {
+                                                       const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
+  seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;                    // [64][HDP] b128 image
@@ -288,7 +289,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
                                                           const T* __restrict__ dout, const float* __restrict__ lse,
                                                           float* __restrict__ Dv, T* __restrict__ dqkv,
                                                           const int* __restrict__ kv_len, int B, int S, int H,
-                                                          float scale, uint64_t seed, uint32_t thr, float inv_keep) {
+                                                          float scale, uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr,
+                                                          float inv_keep) {
+  seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;                                 // K rows, b128 image (A of S^T)
@@ -400,7 +403,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const T* __restrict_
                                                             const float* __restrict__ lse, const float* __restrict__ Dv,
                                                             T* __restrict__ dqkv, const int* __restrict__ kv_len,
                                                             int B, int S, int H, float scale, uint64_t seed,
-                                                            uint32_t thr, float inv_keep) {
+                                                            const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
+  seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Qs = smem;                                   // Q rows b128 image (A of S)
@@ -544,7 +548,7 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
   const int nqt = (S + BQ - 1) / BQ;
   const int smem = G::ROW_BYTES + G::TR_BYTES;
   hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
-                     (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, thr, inv_keep);
+                     (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
 }
 
 template <typename T, int HD>
@@ -556,11 +560,11 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
   const int smem_dq = 2 * G::ROW_BYTES + G::TR_BYTES;
   hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD>), dim3(B * H * nqt), dim3(256), smem_dq, st, (const T*)qkv.data_ptr(),
                      (const T*)o.data_ptr(), (const T*)dout.data_ptr(), lse.data_ptr<float>(),
-                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
+                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
   const int smem_kv = 2 * G::ROW_BYTES + 2 * G::TR_BYTES + 2 * 64 * 4;
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, HD>), dim3(B * H * nkt), dim3(256), smem_kv, st,
                      (const T*)qkv.data_ptr(), (const T*)dout.data_ptr(), lse.data_ptr<float>(),
-                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, thr, inv_keep);
+                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
 }
 
 }  // namespace

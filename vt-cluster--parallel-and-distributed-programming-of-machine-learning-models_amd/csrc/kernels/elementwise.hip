@@ -16,7 +16,9 @@ namespace {
 
 template <typename T>
 __global__ __launch_bounds__(256) void mask_scale_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n,
-                                                         uint64_t seed, uint32_t thr, float inv_keep, int accumulate) {
+                                                         uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep,
+                                                         int accumulate) {
+  seed = mift_seed(seed, sstep);
   const int64_t stride = (int64_t)gridDim.x * 256 * 8;
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += stride) {
     if (i + 8 <= n) {
@@ -52,7 +54,8 @@ MIFT_HD float act_grad(int act, float z) {
 template <typename T>
 __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ g, const T* __restrict__ z,
                                                       T* __restrict__ out, int64_t n, int act, uint64_t seed,
-                                                      uint32_t thr, float inv_keep) {
+                                                      const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
+  seed = mift_seed(seed, sstep);
   const int64_t stride = (int64_t)gridDim.x * 256 * 8;
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += stride) {
     if (i + 8 <= n) {
@@ -80,7 +83,8 @@ template <typename T, typename W>
 __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ pos,
                                                     const W* __restrict__ wte, const W* __restrict__ wpe,
                                                     T* __restrict__ h, int S, int D, int pos_offset,
-                                                    uint64_t seed, uint32_t thr, float inv_keep) {
+                                                    uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
+  seed = mift_seed(seed, sstep);
   const int row = blockIdx.x;
   const int64_t tok = ids[row];
   const int64_t p = (pos != nullptr ? pos[row] : (int64_t)(row % S)) + pos_offset;
@@ -142,7 +146,7 @@ at::Tensor mift_mask_scale(const at::Tensor& x, double p, int64_t seed, const c1
   const int64_t n = x.numel();
   float inv = p > 0 ? mift_inv_keep(p) : 1.f;
   DISPATCH_16(x.scalar_type(), mask_scale_kernel<T><<<ew_grid(n), 256, 0, st>>>((const T*)x.data_ptr(), (T*)y.data_ptr(), n,
-                                                                                 (uint64_t)seed, thr_of(p), inv,
+                                                                                 (uint64_t)seed, mift_seed_step(), thr_of(p), inv,
                                                                                  accumulate ? 1 : 0));
   return y;
 }
@@ -155,7 +159,7 @@ at::Tensor mift_act_bwd(const at::Tensor& g, const at::Tensor& z, int64_t act, d
   float inv = p > 0 ? mift_inv_keep(p) : 1.f;
   DISPATCH_16(g.scalar_type(), act_bwd_kernel<T><<<ew_grid(n), 256, 0, st>>>((const T*)g.data_ptr(), (const T*)z.data_ptr(),
                                                                               (T*)out.data_ptr(), n, (int)act,
-                                                                              (uint64_t)seed, thr_of(p), inv));
+                                                                              (uint64_t)seed, mift_seed_step(), thr_of(p), inv));
   return out;
 }
 
@@ -175,7 +179,7 @@ at::Tensor mift_embed_fwd(const at::Tensor& ids, const c10::optional<at::Tensor>
   DISPATCH_16(out_dtype, embed_kernel<T, T><<<rows, 256, 0, st>>>(
                              ids.data_ptr<int64_t>(), pos ? pos->data_ptr<int64_t>() : nullptr, (const T*)wte.data_ptr(),
                              wpe ? (const T*)wpe->data_ptr() : nullptr, (T*)h.data_ptr(), S, D, (int)pos_offset,
-                             (uint64_t)seed, thr_of(p), inv));
+                             (uint64_t)seed, mift_seed_step(), thr_of(p), inv));
   return h;
 }
 

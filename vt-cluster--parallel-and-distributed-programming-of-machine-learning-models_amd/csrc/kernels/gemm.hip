@@ -67,6 +67,7 @@ struct EpiArgs {
   uint32_t ext_thr;        // != 0: K-extension product is dropout-masked (LoRA input-dropout backward)
   uint64_t ext_seed;
   float ext_inv_keep;
+  const int64_t* sstep;    // device micro-step for graph-replayed dropout seeds (common.h mift_seed)
 };
 
 // Split-K tail (second launch of a hybrid data-parallel + split-K GEMM): the
@@ -132,6 +133,10 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "stage pieces must split evenly over waves");
   constexpr int PER_STAGE = (A_INSTR + B_INSTR) / NW;  // vmcnt units per stage per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (ep.sstep != nullptr) {
+    ep.seed = mift_seed(ep.seed, ep.sstep);
+    ep.ext_seed = mift_seed(ep.ext_seed, ep.sstep);
+  }
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -578,6 +583,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
   ep.ext_thr = mift_thr16(ext_p);
   ep.ext_seed = (uint64_t)ext_seed;
   ep.ext_inv_keep = ext_p > 0 ? mift_inv_keep(ext_p) : 1.f;
+  ep.sstep = mift_seed_step();
   ep.pre_add = nullptr;
   if (pre_add) {
     TORCH_CHECK(pre_add->size(0) == M && pre_add->size(1) == N && pre_add->stride(0) == c.stride(0) &&

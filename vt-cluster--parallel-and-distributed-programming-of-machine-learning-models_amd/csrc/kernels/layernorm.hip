@@ -102,7 +102,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      const float* __restrict__ rstd_in, const T* __restrict__ dres,
                                                      T* __restrict__ dx, T* __restrict__ dbranch,
                                                      float* __restrict__ dw, float* __restrict__ db, int M, int D,
-                                                     uint64_t seed, uint32_t thr, float inv_keep) {
+                                                     uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
+  seed = mift_seed(seed, sstep);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -202,7 +203,7 @@ void ln_bwd_launch(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& 
       (const T*)dy.data_ptr(), (const T*)x.data_ptr(), (const W*)w.data_ptr(), mean.data_ptr<float>(),
       rstd.data_ptr<float>(), dres ? (const T*)dres->data_ptr() : nullptr, (T*)dx.data_ptr(),
       dbranch ? (T*)dbranch->data_ptr() : nullptr, dw ? dw->data_ptr<float>() : nullptr,
-      db ? db->data_ptr<float>() : nullptr, M, D, seed, thr, inv_keep);
+      db ? db->data_ptr<float>() : nullptr, M, D, seed, mift_seed_step(), thr, inv_keep);
 }
 
 template <typename T, typename W>

@@ -67,8 +67,9 @@ MIFT_HD frag_t<T> masked_frag(const T* p, uint64_t seed, uint64_t idx0, uint32_t
 template <typename T>
 __global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X, const T* __restrict__ W,
                                                         T* __restrict__ out, int M, int K, int ldx, float alpha,
-                                                        uint64_t seed, uint32_t thr, float inv_keep, int KS,
+                                                        uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep, int KS,
                                                         float* __restrict__ ws) {
+  seed = mift_seed(seed, sstep);
   __shared__ float red[4][32][33];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, fr = lane & 15;
@@ -183,8 +184,9 @@ MIFT_HD v4s tr_read(const char* lds_base, int off) {
 template <typename T>
 __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X, const T* __restrict__ Y,
                                                          float* __restrict__ out, int M, int P, int ldx,
-                                                         int rows_per_block, uint64_t seed, uint32_t thr,
+                                                         int rows_per_block, uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr,
                                                          float inv_keep, int mode, int rank, int qoff) {
+  seed = mift_seed(seed, sstep);
   // NB 32-row steps per group: the whole group's global loads are in flight
   // together (one 16-B X load + half a Y load per thread per step), staged
   // into NB LDS buffers, then consumed; the next group's loads are issued
@@ -323,11 +325,11 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   if (x.scalar_type() == at::kBFloat16)
     lora_proj_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)x.data_ptr(), (const bf16*)w.data_ptr(),
                                                  (bf16*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                 (uint64_t)seed, thr, ik, KS, ws);
+                                                 (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
   else
     lora_proj_kernel<fp16><<<grid, 256, 0, st>>>((const fp16*)x.data_ptr(), (const fp16*)w.data_ptr(),
                                                  (fp16*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                 (uint64_t)seed, thr, ik, KS, ws);
+                                                 (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
   if (KS > 1) {
     const int rg = (int)(((int64_t)M * 32 / 8 + 255) / 256);
     if (x.scalar_type() == at::kBFloat16)
@@ -362,11 +364,11 @@ void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, 
   if (x.scalar_type() == at::kBFloat16)
     lora_wgrad_kernel<bf16><<<ntp * splits, 256, 0, st>>>((const bf16*)x.data_ptr(), (const bf16*)y.data_ptr(),
                                                           out.data_ptr<float>() + offset, M, P, (int)x.stride(0), rows,
-                                                          (uint64_t)seed, thr, ik, (int)mode, (int)rank, (int)qoff);
+                                                          (uint64_t)seed, mift_seed_step(), thr, ik, (int)mode, (int)rank, (int)qoff);
   else
     lora_wgrad_kernel<fp16><<<ntp * splits, 256, 0, st>>>((const fp16*)x.data_ptr(), (const fp16*)y.data_ptr(),
                                                           out.data_ptr<float>() + offset, M, P, (int)x.stride(0), rows,
-                                                          (uint64_t)seed, thr, ik, (int)mode, (int)rank, (int)qoff);
+                                                          (uint64_t)seed, mift_seed_step(), thr, ik, (int)mode, (int)rank, (int)qoff);
 }
 
 // ------------------------------------------------------------ pack_lora_all

@@ -27,6 +27,13 @@ void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, 
 void mift_pack_lora_all(const at::Tensor& arena, const at::Tensor& table, const at::Tensor& scales, at::Tensor& out,
                         int64_t max_elems);
 
+// ---- row producers fused with the LoRA projection (kernels/rowproj.hip)
+std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
+                                                 double eps, const at::Tensor& pw, int64_t rank, double alpha,
+                                                 double p, int64_t seed);
+std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t seed, const at::Tensor& pw,
+                                       int64_t rank, double alpha);
+
 // ---- elementwise / embedding / LoRA pack (kernels/elementwise.hip)
 at::Tensor mift_mask_scale(const at::Tensor& x, double p, int64_t seed, const c10::optional<at::Tensor>& out,
                            bool accumulate);
@@ -61,6 +68,8 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
 #define MIFT_BIND_MORE(m) \
   m.def("decode_attn", &mift_decode_attn, "single-token attention over a KV cache; appends k/v at t"); \
   m.def("lora_proj", &mift_lora_proj, "out[M,32] = alpha*drop(x)@w^T (tall-skinny MFMA)"); \
+  m.def("layer_norm_fwd_proj", &mift_layer_norm_fwd_proj, "LN fwd + alpha*drop(y)@pw^T -> (y, mean, rstd, proj)"); \
+  m.def("mask_proj", &mift_mask_proj, "y = dropout(x) (p>0), proj = alpha*y@pw^T -> (y, proj)"); \
   m.def("lora_wgrad", &mift_lora_wgrad, "out[P,32] += drop(x)^T @ y (tr_b16 split-M MFMA); arena modes"); \
   m.def("pack_lora_all", &mift_pack_lora_all, "pack every adapter's 16-bit operands from the fp32 arena"); \
   m.def("attn_fwd", &mift_attn_fwd, "causal flash attention fwd on fused qkv -> (o, lse)"); \

@@ -139,6 +139,9 @@ class LoraArena:
 
     def rebind_grads(self):
         """Re-point .grad to the arena (autograd may have replaced it)."""
+        if self.grad.is_cuda:
+            from ..ops.streams import join
+            join()  # side-stream weight-grad kernels (mift.ops.streams) complete before any reader
         for (n, p), o in zip(self.named, self.offsets):
             g = self.grad[o:o + p.numel()].view_as(p)
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():

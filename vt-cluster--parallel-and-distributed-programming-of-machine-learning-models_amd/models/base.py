@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.dispatch import use_kernels
-from .layers import seed_for
+from .layers import dropout_seed, seed_for
 
 
 class CausalLMBase(nn.Module):
@@ -46,7 +46,7 @@ class CausalLMBase(nn.Module):
         self.micro_step += 1
 
     def embed_seed(self):
-        return seed_for(self.seed, self.micro_step, 1)
+        return dropout_seed(self.seed, self.micro_step, 1)
 
     def _use_fused(self, t):
         return self.fused and use_kernels(t)

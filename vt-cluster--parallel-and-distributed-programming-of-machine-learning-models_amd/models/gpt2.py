@@ -19,7 +19,7 @@ import torch.nn as nn
 
 from ..ops import reference as ref
 from .base import CausalLMBase, ref_lm_loss
-from .layers import Embedding, LayerNorm, Linear, init_normal_, padded_vocab, seed_for
+from .layers import Embedding, LayerNorm, Linear, dropout_seed, init_normal_, padded_vocab, seed_for
 
 
 @dataclass
@@ -91,7 +91,7 @@ class GPT2Block(nn.Module):
 
     def site_seeds(self, base, step):
         s = 100 + 10 * self.idx
-        return {k: seed_for(base, step, s + i) for i, k in
+        return {k: dropout_seed(base, step, s + i) for i, k in
                 enumerate(["attn", "attn_out", "mlp_out", "lora_attn", "lora_proj", "lora_mlp"])}
 
     def forward_ref(self, h, seeds, training, key_valid=None, attn=None):

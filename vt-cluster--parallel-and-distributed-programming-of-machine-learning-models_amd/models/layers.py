@@ -199,6 +199,24 @@ def seed_for(base: int, step: int, site: int) -> int:
     return x & ((1 << 63) - 1)
 
 
+_GRAPH_SEEDS = [False]
+
+
+def graph_seeds(on: bool):
+    """Switch dropout-site seeds to their step-free form for hipGraph capture (mift.train.graph)."""
+    _GRAPH_SEEDS[0] = bool(on)
+
+
+def dropout_seed(base: int, step: int, site: int) -> int:
+    """Seed of a dropout site = ``seed_for(base, step, site)``.  Under hipGraph capture the step is
+    read on the device instead (csrc/common.h ``mift_seed``): return the signed 64-bit
+    ``base*C1 + site*C3`` and let every replay add its own micro-step."""
+    if _GRAPH_SEEDS[0]:
+        x = (base * 0x9E3779B97F4A7C15 + site * 0x94D049BB133111EB) & ((1 << 64) - 1)
+        return x - (1 << 64) if x >= (1 << 63) else x
+    return seed_for(base, step, site)
+
+
 def name_generator(seed: int, name: str, device=None) -> torch.Generator:
     """RNG keyed by (seed, parameter name): a pipeline stage that builds only some
     layers draws exactly the values the full model would (stage-local init)."""

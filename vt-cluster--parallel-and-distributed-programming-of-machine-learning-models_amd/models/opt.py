@@ -32,7 +32,7 @@ import torch.nn as nn
 
 from ..ops import reference as ref
 from .base import CausalLMBase, ref_lm_loss, shift_labels
-from .layers import ConcatLinear, Embedding, LayerNorm, Linear, init_normal_, padded_vocab, seed_for
+from .layers import ConcatLinear, Embedding, LayerNorm, Linear, dropout_seed, init_normal_, padded_vocab, seed_for
 
 
 @dataclass
@@ -118,7 +118,7 @@ class OPTDecoderLayer(nn.Module):
 
     def site_seeds(self, base, step):
         s = 100 + 10 * self.idx
-        return {k: seed_for(base, step, s + i) for i, k in enumerate(self.SITES)}
+        return {k: dropout_seed(base, step, s + i) for i, k in enumerate(self.SITES)}
 
     def forward_ref(self, h, seeds, training, key_valid=None, attn=None):
         """h: [B, S, d] (reference path).  One LoRA-dropout seed for q/k/v (see MultiAdapterOps).

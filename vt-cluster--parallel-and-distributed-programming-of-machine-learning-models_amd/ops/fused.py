@@ -26,6 +26,7 @@ variant used by OPT's fused q/k/v projection — mift.models.opt).
 import torch
 
 from . import kernels as K
+from .streams import run_side
 
 _BWD = {0: 0, 1: 4, 2: 5, 3: 6}
 
@@ -39,6 +40,7 @@ class AdapterOps:
 
     def __init__(self, lin, dtype):
         self.r, self.s, self.p = lin.lora_r, lin.lora_scaling, lin.lora_dropout
+        self.rows, self.dt_alpha = self.r, self.s  # non-zero rows of A32s / B32t; dT = dt_alpha·gz·B32tᵀ
         pk = getattr(lin, "_pack_owner", None)
         self.arena = getattr(lin, "_arena", None)
         if self.arena is not None:
@@ -59,15 +61,21 @@ class AdapterOps:
         """T32 = s·dropout(x)·A^T  [M,32] (mask applied in-register, never stored)."""
         return K.lora_proj(x, self.A32s, 1.0, self.p if training else 0.0, seed)
 
-    def backward(self, gz, x, T32, seed, training):
-        """-> (grads for lora_params() [dA, dB] or [None, None], dT32)."""
+    def backward(self, gz, x, T32, seed, training, dT32=None):
+        """-> (grads for lora_params() [dA, dB] or [None, None], dT32).
+
+        ``dT32`` may come precomputed from the kernel that produced gz (mask_proj)."""
         r = self.r
         p = self.p if training else 0.0
-        dT32 = K.lora_proj(gz, self.B32t, self.s, 0.0, 0)            # s·gz·B   [M,32]
+        if dT32 is None:
+            dT32 = K.lora_proj(gz, self.B32t, self.s, 0.0, 0)        # s·gz·B   [M,32]
         if self.arena is not None:
-            g = self.arena.grad
-            K.lora_wgrad_into(gz, T32, g, 1, r, self.offB)             # dB [N,r]
-            K.lora_wgrad_into(x, dT32, g, 2, r, self.offA, p, seed)    # dA [r,K]
+            g, offA, offB = self.arena.grad, self.offA, self.offB
+
+            def wgrad():
+                K.lora_wgrad_into(gz, T32, g, 1, r, offB)              # dB [N,r]
+                K.lora_wgrad_into(x, dT32, g, 2, r, offA, p, seed)     # dA [r,K]
+            run_side(gz.device, wgrad, gz, T32, x, dT32)
             return [None, None], dT32
         dBf = K.lora_wgrad(gz, T32)
         dAf = K.lora_wgrad(x, dT32, p=p, seed=seed)
@@ -94,6 +102,8 @@ class MultiAdapterOps:
         members = [(l, n0, n1) for l, n0, n1 in cat.spans() if l.lora_r > 0]
         self.w = 32 // len(members)
         self.slots = [(l, n0, n1, j * self.w) for j, (l, n0, n1) in enumerate(members)]
+        self.rows = max(q + l.lora_r for l, _, _, q in self.slots)
+        self.dt_alpha = 1.0  # s_j baked into B_extT
         first = members[0][0]
         self.p = first.lora_dropout
         self.arena = getattr(first, "_arena", None)
@@ -124,17 +134,20 @@ class MultiAdapterOps:
     def forward(self, x, seed, training):
         return K.lora_proj(x, self.A32s, 1.0, self.p if training else 0.0, seed)
 
-    def backward(self, gz, x, T32, seed, training):
+    def backward(self, gz, x, T32, seed, training, dT32=None):
         p = self.p if training else 0.0
-        dT32 = K.lora_proj(gz, self.B32t, 1.0, 0.0, 0)
+        if dT32 is None:
+            dT32 = K.lora_proj(gz, self.B32t, 1.0, 0.0, 0)
         grads = []
         if self.arena is not None:
-            g = self.arena.grad
-            for l, n0, n1, q in self.slots:
-                K.lora_wgrad_into(gz[:, n0:n1], T32, g, 1, l.lora_r, l._offB, qoff=q)
-                K.lora_wgrad_into(x, dT32, g, 2, l.lora_r, l._offA, p, seed, qoff=q)
-                grads += [None, None]
-            return grads, dT32
+            g, slots = self.arena.grad, self.slots
+
+            def wgrad():
+                for l, n0, n1, q in slots:
+                    K.lora_wgrad_into(gz[:, n0:n1], T32, g, 1, l.lora_r, l._offB, qoff=q)
+                    K.lora_wgrad_into(x, dT32, g, 2, l.lora_r, l._offA, p, seed, qoff=q)
+            run_side(gz.device, wgrad, gz, T32, x, dT32)
+            return [None, None] * len(slots), dT32
         dAf = K.lora_wgrad(x, dT32, p=p, seed=seed)
         for l, n0, n1, q in self.slots:
             dBf = K.lora_wgrad(gz[:, n0:n1], T32)
@@ -164,9 +177,13 @@ class LnLinear(torch.autograd.Function):
     def forward(ctx, x, ln_w, ln_b, lin, eps, lora_seed, training, *lparams):
         shp = x.shape
         x2 = _flat(x.contiguous())
-        a, mean, rstd = K.layer_norm_fwd(x2, ln_w, ln_b, eps)
         lo = lin.lora_ops(x.dtype) if lparams else None
-        T32 = lo.forward(a, lora_seed, training) if lo is not None else None
+        if lo is not None:  # LN and the LoRA input projection in one row pass (csrc/kernels/rowproj.hip)
+            a, mean, rstd, T32 = K.layer_norm_fwd_proj(x2, ln_w, ln_b, eps, lo.A32s, lo.rows, 1.0,
+                                                       lo.p if training else 0.0, lora_seed)
+        else:
+            a, mean, rstd = K.layer_norm_fwd(x2, ln_w, ln_b, eps)
+            T32 = None
         y = K.gemm(a, lin.w_nk(), lin.bias, T32, lo.B32 if lo else None)
         ctx.save_for_backward(x2, a, mean, rstd, ln_w, T32)
         ctx.lin, ctx.lo, ctx.seed, ctx.training, ctx.shp, ctx.nl = lin, lo, lora_seed, training, shp, len(lparams)
@@ -208,8 +225,12 @@ class LinearResidual(torch.autograd.Function):
         x2, T32 = ctx.saved_tensors
         lin, lo = ctx.lin, ctx.lo
         gh2 = _flat(gh.contiguous())
-        gz = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
-        lg, dT32 = (lo.backward(gz, x2, T32, ctx.lseed, ctx.training) if lo is not None else (_nones(ctx.nl), None))
+        if lo is not None:  # residual-dropout backward and dT = s·gz·B in one row pass
+            gz, dT0 = K.mask_proj(gh2, ctx.p, ctx.seed, lo.B32t, lo.rows, lo.dt_alpha)
+            lg, dT32 = lo.backward(gz, x2, T32, ctx.lseed, ctx.training, dT32=dT0)
+        else:
+            gz = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
+            lg, dT32 = _nones(ctx.nl), None
         dx = _dgrad(gz, lin, lo, dT32, ctx.lseed, ctx.training)
         return (dx.view(ctx.xshp), gh, None, None, None, None, None, *lg)
 
@@ -245,11 +266,13 @@ class MLP(torch.autograd.Function):
         h2, a, mean, rstd, ln_w, z, f, T1, T2 = ctx.saved_tensors
         fc1, fc2, lo1, lo2 = ctx.fc1, ctx.fc2, ctx.lo1, ctx.lo2
         gh2 = _flat(gh.contiguous())
-        gm = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
         lg1, lg2 = _nones(ctx.n1), _nones(ctx.n2)
         dT1 = dT2 = None
-        if lo2 is not None:
-            lg2, dT2 = lo2.backward(gm, f, T2, ctx.sl2, ctx.training)
+        if lo2 is not None:  # residual-dropout backward fused with dT2 = s·gm·B2
+            gm, dT0 = K.mask_proj(gh2, ctx.p, ctx.seed, lo2.B32t, lo2.rows, lo2.dt_alpha)
+            lg2, dT2 = lo2.backward(gm, f, T2, ctx.sl2, ctx.training, dT32=dT0)
+        else:
+            gm = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
         # dZ = (gm·W2 [+ masked LoRA ext]) ⊙ act'(z), all in the dgrad epilogue
         dz = _dgrad(gm, fc2, lo2, dT2, ctx.sl2, ctx.training, act=_BWD[ctx.act], aux=z)
         if lo1 is not None:

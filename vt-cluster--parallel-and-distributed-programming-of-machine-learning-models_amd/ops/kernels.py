@@ -73,3 +73,13 @@ def xent(logits, labels, V, ignore_index=-100, write_grad=True):
 def decode_attn(qkv, kcache, vcache, t, scale, start=None):
     """o [B, H*hd] for the token at position t; writes its k/v into the caches."""
     return C().decode_attn(qkv, kcache, vcache, int(t), float(scale), start)
+
+
+def layer_norm_fwd_proj(x, w, b, eps, pw, rank, alpha=1.0, p=0.0, seed=0):
+    """(y, mean, rstd, proj[M,32]) = LN(x), alpha·dropout(y)·pwᵀ — LN fused with the LoRA projection."""
+    return C().layer_norm_fwd_proj(x, w, b, float(eps), pw, int(rank), float(alpha), float(p), int(seed))
+
+
+def mask_proj(x, p, seed, pw, rank, alpha=1.0):
+    """(y, proj[M,32]) = dropout(x) (x itself when p == 0), alpha·y·pwᵀ — dropout-bwd fused with dT."""
+    return C().mask_proj(x, float(p), int(seed), pw, int(rank), float(alpha))

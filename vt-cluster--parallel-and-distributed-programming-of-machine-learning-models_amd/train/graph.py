@@ -1,0 +1,136 @@
+"""hipGraph capture of the training step (MI355X: HIP graphs instead of a tracing compiler).
+
+A distilgpt2 LoRA optimizer step is ~250 kernel launches in ~6 ms of GPU
+time, and issuing them from Python through autograd costs about as much host
+time as the GPU spends executing them, so the eager step is host-bound and
+every kernel speed-up is lost.  ``GraphedStep`` captures the forward and
+backward of all micro-batches of a step — LoRA packing, fused kernels,
+hipBLASLt LM head, the LoRA weight-gradient kernels forked onto a side
+stream (mift.ops.streams) and joined back — into ONE hipGraph and replays it:
+one host launch per step, no inter-kernel gaps, and the side-stream overlap
+for free.
+
+What stays outside the graph (per step, on the host stream):
+  * staging the micro-batches into the graph's static input buffers
+    (async copies from pinned host memory);
+  * the per-step scalars as device tensors: 1/global-token-count and the
+    micro-step counters that every dropout kernel mixes into its seed
+    (``mift_seed`` in csrc/common.h; ``dropout_seed`` in models/layers.py) —
+    so replays draw fresh masks, bit-identical to the eager path;
+  * the DP gradient all-reduce (RCCL), the grad-norm / clip / AdamW kernels
+    and the LR update: a handful of launches, kept eager so collectives are
+    never captured.
+
+Captures are keyed by the micro-batch shapes (the last, shorter step of an
+epoch gets its own graph or runs eagerly); the first step of every shape runs
+eagerly as warm-up (lazy library init, workspace allocation).
+"""
+import os
+
+import torch
+
+from ..models.layers import graph_seeds
+from ..ops import streams
+
+
+class GraphedStep:
+    def __init__(self, trainer, max_graphs: int = 3):
+        self.tr = trainer
+        self.graphs = {}      # signature -> dict(graph, static, steps_t, loss)
+        self.seen = set()     # signatures already run eagerly once (warm-up)
+        self.max_graphs = max_graphs
+        dev = trainer.device
+        self.inv_ntok = torch.ones(1, dtype=torch.float32, device=dev)
+        self.pool = None
+
+    @staticmethod
+    def signature(mbs):
+        return tuple((k, tuple(v.shape), v.dtype) for mb in mbs for k, v in sorted(mb.items()))
+
+    def supported(self, mbs):
+        sig = self.signature(mbs)
+        if sig in self.graphs:
+            return True
+        if sig not in self.seen:
+            self.seen.add(sig)
+            return False  # eager warm-up for this shape
+        return len(self.graphs) < self.max_graphs
+
+    # ------------------------------------------------------------------
+    def _fwd_bwd(self, ent, n):
+        """The captured region: forward + backward of every micro-batch."""
+        tr, model = self.tr, self.tr.model
+        C = _C()
+        ent["loss"].zero_()
+        gscale = tr.opt.loss_scale_t * self.inv_ntok
+        for i in range(n):
+            C.set_seed_step(ent["steps_t"][i:i + 1])
+            mb = ent["static"][i]
+            out = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"], labels=mb["labels"],
+                        reduction="sum", return_logits=False)
+            loss_sum = out["loss"].float()
+            (loss_sum * gscale).backward()
+            streams.join()
+            ent["loss"].add_(loss_sum.detach())
+        C.set_seed_step(None)
+
+    def _capture(self, sig, mbs):
+        tr, model = self.tr, self.tr.model
+        dev = tr.device
+        static = [{k: torch.empty_like(v, device=dev) for k, v in mb.items()} for mb in mbs]
+        ent = {"static": static, "loss": torch.zeros((), dtype=torch.float32, device=dev),
+               "steps_t": torch.zeros(len(mbs), dtype=torch.int64, device=dev),
+               "arange": torch.arange(1, len(mbs) + 1, dtype=torch.int64, device=dev)}
+        for i, mb in enumerate(mbs):
+            for k, v in mb.items():
+                static[i][k].copy_(v)
+        # force the per-step LoRA operand packing into the captured region
+        pk = getattr(model, "_lora_pack", None)
+        if pk is not None:
+            pk.version = -1
+        for m in model.modules():
+            if hasattr(m, "_mpack"):
+                m._mpack = None
+        g = torch.cuda.CUDAGraph()
+        ms0 = model.micro_step
+        torch.cuda.synchronize()
+        graph_seeds(True)
+        streams.set_enabled(os.environ.get("MIFT_GRAPH_SIDE", "1") != "0")
+        try:
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
+                self._fwd_bwd(ent, len(mbs))
+        finally:
+            graph_seeds(False)
+            streams.set_enabled(None)
+            _C().set_seed_step(None)
+            model.micro_step = ms0
+        if self.pool is None:
+            self.pool = g.pool()
+        ent["graph"] = g
+        self.graphs[sig] = ent
+        return ent
+
+    # ------------------------------------------------------------------
+    def run(self, mbs, ntok):
+        """Forward + backward of one optimizer step by graph replay; returns the summed loss tensor."""
+        tr, model = self.tr, self.tr.model
+        sig = self.signature(mbs)
+        ent = self.graphs.get(sig)
+        fresh = ent is None
+        if fresh:
+            ent = self._capture(sig, mbs)
+        else:
+            for i, mb in enumerate(mbs):
+                for k, v in mb.items():
+                    ent["static"][i][k].copy_(v, non_blocking=True)
+        self.inv_ntok.fill_(1.0 / float(ntok))
+        n = len(mbs)
+        torch.add(ent["arange"], model.micro_step, out=ent["steps_t"])
+        ent["graph"].replay()
+        model.micro_step += n
+        return ent["loss"]
+
+
+def _C():
+    from ..ops.dispatch import C
+    return C()

@@ -59,6 +59,7 @@ class TrainConfig:
     zero_stage: int = 0                # 1: shard AdamW state over the DP group (mift.parallel.zero)
     trainable: str = "lora"            # lora | all (full fine-tuning: the tiny-BERT lab)
     logging_first_step: bool = False
+    graph: str = "off"                 # hipGraph-replayed steps (mift.train.graph): on | off (MIFT_GRAPH)
 
 
 class Trainer:
@@ -113,6 +114,21 @@ class Trainer:
         if hasattr(model, "recompute"):
             model.recompute = cfg.recompute
         self._ctrl = ctx.ctrl_group if ctx else None
+        self.graphed = None
+        if self._graph_ok():
+            from .graph import GraphedStep
+            self.graphed = GraphedStep(self)
+
+    def _graph_ok(self):
+        mode = os.environ.get("MIFT_GRAPH", self.cfg.graph)
+        if mode in ("off", "0", "false", False, "", None) or self.device.type != "cuda":
+            return False
+        from ..ops.dispatch import use_kernels
+        ok = (getattr(self.model, "fused", False) and use_kernels(self.arena.param) and self.pp == 1
+              and self.cfg.trainable == "lora" and not self.cfg.recompute and hasattr(self.model, "micro_step"))
+        if mode in ("on", "1", "true", True) and not ok:
+            raise RuntimeError("graph=on needs the fused GPU LoRA path without pipeline / recompute")
+        return ok
 
     # ------------------------------------------------------------------
     def _global_tokens(self, mbs):
@@ -151,6 +167,8 @@ class Trainer:
         ntok = self._global_tokens(mbs)
         lr = self.sched(self.global_step)
         self.opt.set_lr(lr)
+        if self.graphed is not None and self.graphed.supported(mbs):
+            return self._finish_step(self.graphed.run(mbs, ntok), ntok)
         gscale = self.opt.loss_scale_t / ntok
         if self.engine is not None:
             dev_mbs = [self._to_dev(mb) for mb in mbs]
