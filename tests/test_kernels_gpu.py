@@ -188,10 +188,11 @@ def test_flash_attention_kv_len():
 
 
 @pytest.mark.parametrize("p", [0.0, 0.05])
-def test_lora_proj_and_wgrad(p):
+@pytest.mark.parametrize("K", [768, 3072])
+def test_lora_proj_and_wgrad(p, K):
     C = _C()
     torch.manual_seed(8)
-    M, K = 1000, 768
+    M = 1000
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.zeros(32, K, device="cuda", dtype=torch.bfloat16)
     w[:8] = (torch.randn(8, K, device="cuda") * 0.05).to(torch.bfloat16)

@@ -110,20 +110,26 @@ static inline float mift_inv_keep(double p) {
   return t >= 65536u ? 0.f : (float)(65536.0 / (65536.0 - (double)t));
 }
 
-// GPT-2 "gelu_new" (tanh approximation) and its derivative.
-// tanh via one v_exp_f32 + one fast divide (saturates correctly at +-inf)
-MIFT_HD float fast_tanh(float u) { return 1.f - __fdividef(2.f, 1.f + __expf(2.f * u)); }
-MIFT_HD float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + fast_tanh(u));
+// GPT-2 "gelu_new" (tanh approximation) and its derivative, in the sigmoid form
+//   0.5·x·(1 + tanh(u)) = x·σ(2u),  u = k0·(x + k1·x³)
+// = x / (1 + 2^(x·(c0 + c1·x²))): one v_exp_f32 + one v_rcp_f32 + 4 FMA-class ops
+// (the tanh form needed an extra divide/negate chain; the MLP GEMM epilogues apply it to
+// 25 M elements per layer, where it was the dominant VALU cost).  Saturates correctly:
+// x -> -inf gives 2^+inf = inf -> σ = 0; x -> +inf gives σ = 1.
+MIFT_HD float gelu_sig(float x, float x2) {
+  constexpr float c0 = -2.3022081983f;    // -2·k0·log2(e)
+  constexpr float c1 = -0.1029432396f;    // c0·k1
+  const float e = __builtin_amdgcn_exp2f(x * __builtin_fmaf(c1, x2, c0));
+  return __builtin_amdgcn_rcpf(1.f + e);
 }
+MIFT_HD float fast_tanh(float u) { return 1.f - __fdividef(2.f, 1.f + __expf(2.f * u)); }
+MIFT_HD float gelu_tanh(float x) { return x * gelu_sig(x, x * x); }
 MIFT_HD float gelu_tanh_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = fast_tanh(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  // d/dx x·σ(2u) = σ + x·σ(1-σ)·2u',  2u' = 2k0·(1 + 3k1·x²)
+  constexpr float c2 = 1.5957691216057308f, c3 = 0.2140644488f;  // 2k0, 6·k0·k1
+  const float x2 = x * x;
+  const float s = gelu_sig(x, x2);
+  return __builtin_fmaf(x * s * (1.f - s), __builtin_fmaf(c3, x2, c2), s);
 }
 MIFT_HD float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 MIFT_HD float gelu_erf_grad(float x) {

@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
 
 // ========================== backward: dK, dV ===============================
 template <typename T, int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+__global__ __launch_bounds__(256, HD <= 64 ? 3 : 1) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ Dv,
                                                             T* __restrict__ dqkv, const int* __restrict__ kv_len,
                                                             int B, int S, int H, float scale, uint64_t seed,

@@ -308,8 +308,20 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
           if (full) load8<T>(reinterpret_cast<const T*>(ep.aux) + off, ax);
           else for (int e = 0; e < N - gc; ++e) ax[e] = (float)reinterpret_cast<const T*>(ep.aux)[off + e];
         }
+        // one uniform branch per 8 elements (not a switch per element)
+        switch (ep.act) {
+          case ACT_GELU_TANH:
   #pragma unroll
-        for (int e = 0; e < 8; ++e) z[e] = apply_act(ep.act, z[e], ax[e]);
+            for (int e = 0; e < 8; ++e) z[e] = gelu_tanh(z[e]);
+            break;
+          case ACT_GELU_TANH_BWD:
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) z[e] *= gelu_tanh_grad(ax[e]);
+            break;
+          default:
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) z[e] = apply_act(ep.act, z[e], ax[e]);
+        }
       }
       if (ep.thr != 0) {
         bool kp[8];

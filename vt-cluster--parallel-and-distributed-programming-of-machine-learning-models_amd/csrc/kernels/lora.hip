@@ -64,13 +64,13 @@ MIFT_HD frag_t<T> masked_frag(const T* p, uint64_t seed, uint64_t idx0, uint32_t
 // partial to ws[kss] with plain stores and lora_proj_reduce sums the KS
 // partials into the 16-bit output (an in-kernel last-block reduction needs a
 // device-scope fence per block, ~3.5 us on gfx950 — slower than a launch).
-template <typename T>
-__global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X, const T* __restrict__ W,
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict__ X, const T* __restrict__ W,
                                                         T* __restrict__ out, int M, int K, int ldx, float alpha,
                                                         uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep, int KS,
                                                         float* __restrict__ ws) {
   seed = mift_seed(seed, sstep);
-  __shared__ float red[4][32][33];
+  __shared__ float red[NW][32][33];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, fr = lane & 15;
   const int mb = blockIdx.x / KS, kss = blockIdx.x % KS;
@@ -86,9 +86,10 @@ __global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X,
   const int kb0 = kss * per_blk, nks = min(nks_all, kb0 + per_blk);
   // each wave owns a contiguous K range of the block's split; UNR k-steps of
   // loads are issued back to back before their MFMAs (memory-level
-  // parallelism: one 16-B load per lane per operand per k-step)
+  // parallelism: one 16-B load per lane per operand per k-step).  NW = 8 for
+  // long K halves every wave's chain of dependent load rounds.
   constexpr int UNR = 4;
-  const int per = (nks - kb0 + 3) / 4;
+  const int per = (nks - kb0 + NW - 1) / NW;
   const int kbeg = kb0 + wave * per, kend = min(nks, kbeg + per);
   for (int ks0 = kbeg; ks0 < kend; ks0 += UNR) {
     short8 ra[UNR][2], rb[UNR][2];
@@ -138,18 +139,23 @@ __global__ __launch_bounds__(256) void lora_proj_kernel(const T* __restrict__ X,
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wave][i * 16 + g * 4 + r][j * 16 + fr] = acc[i][j][r];
   __syncthreads();
+  auto rsum = [&](int r, int c) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][r][c];
+    return v;
+  };
   if (KS == 1) {
-    for (int e = tid; e < 32 * 32; e += 256) {
+    for (int e = tid; e < 32 * 32; e += NW * 64) {
       const int r = e >> 5, c = e & 31;
-      const float v = (red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c]) * alpha;
-      if (m0 + r < M) out[(int64_t)(m0 + r) * 32 + c] = (T)v;
+      if (m0 + r < M) out[(int64_t)(m0 + r) * 32 + c] = (T)(rsum(r, c) * alpha);
     }
     return;
   }
   float* wp = ws + (int64_t)kss * M * 32;
-  for (int e = tid; e < 32 * 32; e += 256) {
+  for (int e = tid; e < 32 * 32; e += NW * 64) {
     const int r = e >> 5, c = e & 31;
-    if (m0 + r < M) wp[(int64_t)(m0 + r) * 32 + c] = red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c];
+    if (m0 + r < M) wp[(int64_t)(m0 + r) * 32 + c] = rsum(r, c);
   }
 }
 
@@ -322,14 +328,21 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
     ws = wsb.data_ptr<float>();
   }
   const int grid = mblocks * KS;
-  if (x.scalar_type() == at::kBFloat16)
-    lora_proj_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)x.data_ptr(), (const bf16*)w.data_ptr(),
-                                                 (bf16*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                 (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
-  else
-    lora_proj_kernel<fp16><<<grid, 256, 0, st>>>((const fp16*)x.data_ptr(), (const fp16*)w.data_ptr(),
-                                                 (fp16*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                 (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
+  // 8 waves per row block when each of 4 waves would walk > 8 k-steps (K/KS > 1024)
+  const bool wide = nks / KS > 32;
+  auto go = [&](auto tt) {
+    using T = decltype(tt);
+    if (wide)
+      lora_proj_kernel<T, 8><<<grid, 512, 0, st>>>((const T*)x.data_ptr(), (const T*)w.data_ptr(),
+                                                   (T*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
+                                                   (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
+    else
+      lora_proj_kernel<T, 4><<<grid, 256, 0, st>>>((const T*)x.data_ptr(), (const T*)w.data_ptr(),
+                                                   (T*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
+                                                   (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
+  };
+  if (x.scalar_type() == at::kBFloat16) go(bf16{});
+  else go(fp16{});
   if (KS > 1) {
     const int rg = (int)(((int64_t)M * 32 / 8 + 255) / 256);
     if (x.scalar_type() == at::kBFloat16)

@@ -1,14 +1,17 @@
 """hipGraph capture of the training step (MI355X: HIP graphs instead of a tracing compiler).
 
 A distilgpt2 LoRA optimizer step is ~250 kernel launches in ~6 ms of GPU
-time, and issuing them from Python through autograd costs about as much host
-time as the GPU spends executing them, so the eager step is host-bound and
-every kernel speed-up is lost.  ``GraphedStep`` captures the forward and
+time; issuing them from Python through autograd costs ~2.8 ms of host time
+per step (tools/graph_overhead.py), 0.17 ms as a graph replay.  The eager
+step is therefore GPU-bound today, but the host cost becomes the limit as the
+kernels get faster, with more micro-batches per step, and for small decode
+steps.  ``GraphedStep`` captures the forward and
 backward of all micro-batches of a step — LoRA packing, fused kernels,
-hipBLASLt LM head, the LoRA weight-gradient kernels forked onto a side
-stream (mift.ops.streams) and joined back — into ONE hipGraph and replays it:
-one host launch per step, no inter-kernel gaps, and the side-stream overlap
-for free.
+hipBLASLt LM head — into ONE hipGraph and replays it: one host launch per
+step and no inter-kernel gaps.  ``MIFT_GRAPH_SIDE=1`` also forks the LoRA
+weight-gradient kernels onto a side stream inside the graph (mift.ops.streams);
+measured on MI355X it slows the co-running dgrad GEMMs more than it hides
+(device 6.18 vs 5.99 ms/step, tools/graph_overhead.py), so it is off.
 
 What stays outside the graph (per step, on the host stream):
   * staging the micro-batches into the graph's static input buffers
@@ -95,7 +98,7 @@ class GraphedStep:
         ms0 = model.micro_step
         torch.cuda.synchronize()
         graph_seeds(True)
-        streams.set_enabled(os.environ.get("MIFT_GRAPH_SIDE", "1") != "0")
+        streams.set_enabled(os.environ.get("MIFT_GRAPH_SIDE", "0") == "1")
         try:
             with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
                 self._fwd_bwd(ent, len(mbs))
