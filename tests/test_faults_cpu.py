@@ -61,3 +61,34 @@ def test_resume_auto_is_exact(tmp_path):
     assert sa.keys() == sb.keys()
     for k in sa:
         torch.testing.assert_close(sa[k], sb[k], atol=1e-6, rtol=1e-5)
+
+
+def _diverge_worker(rank, world):
+    import torch
+    from mift import lora as L
+    from mift.data import MicroBatcher, synthetic_openwebtext
+    from mift.models import build_causal_lm
+    from mift.parallel import dist as D
+    from mift.train.trainer import TrainConfig, Trainer
+
+    ctx = D.init(verbose=False, sanity=False)
+    model = build_causal_lm("opt-tiny", seed=3)
+    if rank == 1:  # a replica that loaded different weights
+        with torch.no_grad():
+            next(p for p in model.parameters()).add_(0.5)
+    L.inject(model, L.LoraConfig(r=4, lora_alpha=8, target_modules=["q_proj", "v_proj"]), seed=3)
+    ds = synthetic_openwebtext(16, 8, model.config.vocab_size, model.config.pad_token_id, seed=5)
+    try:
+        Trainer(model, MicroBatcher(ds, 2, 2, rank=ctx.dp_rank, world=ctx.dp),
+                TrainConfig(precision="fp32", step_log="none", logging_steps=0, save_steps=0), ctx)
+        return "no-error"
+    except RuntimeError as e:
+        return "diverged" if "replica divergence" in str(e) else repr(e)
+    finally:
+        D.destroy()
+
+
+def test_replica_divergence_detected():
+    """DP replicas are not broadcast at start (identical init by seed); a checksum all-reduce
+    over the DP group must catch a replica whose weights differ."""
+    assert harness.run(_diverge_worker, 2) == ["diverged", "diverged"]

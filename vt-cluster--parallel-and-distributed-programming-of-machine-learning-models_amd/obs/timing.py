@@ -62,6 +62,14 @@ def p2_loss_line(rank, ep, step, loss, dt):
     return f"[R{rank}] ep={ep} step={step} loss={loss:.4f} (+{dt:.1f}s)"
 
 
+def perf_line(rank, step, tokens_per_sec, tflops, hbm_gb, comm_ms, world):
+    """MI355X additions to the reference metrics: whole-job padded tokens/s, model
+    TFLOP/s per GPU (6·N·T-style estimate, LoRA: no base weight grads), peak HBM per rank and the
+    gradient all-reduce time of the last step."""
+    return (f"[perf] rank={rank} step={step} world={world} tokens_per_sec={tokens_per_sec:.1f} "
+            f"tflops_per_gpu={tflops:.1f} hbm_gb={hbm_gb:.2f} comm_ms={comm_ms:.3f}")
+
+
 def hf_log_line(d: dict):
     """Trainer-style ``{'loss': ..., 'learning_rate': ..., 'epoch': ...}``."""
     return str({k: (round(v, 4) if (isinstance(v, float) and k in ("loss", "grad_norm", "epoch")) else v)

@@ -29,8 +29,8 @@ import torch
 import torch.distributed as dist
 
 from ..lora import LoraArena, adapter_state_dict, save_adapter
-from ..obs.timing import HOST, hf_log_line, lab_step_line, p1_step_line
-from ..parallel.ddp import GradReducer
+from ..obs.timing import HOST, hf_log_line, lab_step_line, p1_step_line, perf_line
+from ..parallel.ddp import GradReducer, verify_replicas
 from ..utils.faults import maybe_inject
 from .optim import FusedAdamW, linear_schedule
 
@@ -60,6 +60,7 @@ class TrainConfig:
     trainable: str = "lora"            # lora | all (full fine-tuning: the tiny-BERT lab)
     logging_first_step: bool = False
     graph: str = "off"                 # hipGraph-replayed steps (mift.train.graph): on | off (MIFT_GRAPH)
+    consistency_every: int = 0         # >0: checksum the trainable params across DP replicas every N steps
 
 
 class Trainer:
@@ -118,6 +119,13 @@ class Trainer:
         if self._graph_ok():
             from .graph import GraphedStep
             self.graphed = GraphedStep(self)
+        self._comm_ev = None
+        self._tok_seen = 0
+        if self.dp > 1 and dist.is_initialized():
+            # replaces DDP's construction broadcast (reference X6): identical init by seed,
+            # verified with one checksum all-reduce over the DP group
+            verify_replicas([self.arena.param] + [p.detach() for p in model.parameters() if not p.requires_grad],
+                            group=self.dp_group)
 
     def _graph_ok(self):
         mode = os.environ.get("MIFT_GRAPH", self.cfg.graph)
@@ -196,10 +204,17 @@ class Trainer:
 
     def _finish_step(self, loss_acc, ntok):
         self.arena.rebind_grads()
+        timed = self.device.type == "cuda" and self.dp > 1
+        if timed:
+            if self._comm_ev is None:
+                self._comm_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self._comm_ev[0].record()
         if self.zero:
             self.opt.reduce_grads()
         else:
             self.reducer.finish()
+        if timed:
+            self._comm_ev[1].record()
         self.opt.step()
         self.arena.bump()
         self.global_step += 1
@@ -222,6 +237,7 @@ class Trainer:
             start_step = self.resume(cfg.resume)
         self.model.train()
         t_last = time.perf_counter()
+        self._perf_t0, self._tok_seen = t_last, 0
         sync_dev = self.device.type == "cuda"
         epoch = start_step // max(1, self.steps_per_epoch)
         done = start_step >= self.total_steps
@@ -245,7 +261,11 @@ class Trainer:
                         sps = samples / max(dt, 1e-9)
                         seq = mbs[0]["input_ids"].shape[1]
                         print(lab_step_line(self.rank, self.global_step, dt * 1000, sps, sps * seq), flush=True)
+                self._tok_seen += sum(int(mb["input_ids"].numel()) for mb in mbs) * self.dp
+                if cfg.consistency_every and self.dp > 1 and self.global_step % cfg.consistency_every == 0:
+                    verify_replicas([self.arena.param], group=self.dp_group)
                 if log_now:
+                    self._perf_log(mbs)
                     st = self.opt.stats()
                     rec = {"loss": self._loss_for_log(loss_sum) / max(1, ntok),
                            "grad_norm": st["grad_norm"], "learning_rate": self.sched(self.global_step),
@@ -269,6 +289,28 @@ class Trainer:
         if sync_dev:
             torch.cuda.synchronize()
         return self.history
+
+    def _perf_log(self, mbs):
+        if self.rank != 0:
+            self._tok_seen, self._perf_t0 = 0, time.perf_counter()
+            return
+        now = time.perf_counter()
+        t0 = getattr(self, "_perf_t0", None)
+        self._perf_t0 = now
+        toks, self._tok_seen = self._tok_seen, 0
+        if t0 is None or now <= t0:
+            return
+        tps = toks / (now - t0)
+        n = getattr(self.model, "num_flop_params", None)
+        nparams = n() if callable(n) else sum(p.numel() for p in self.model.parameters())
+        tflops = 4.0 * nparams * tps / max(1, self.ctx.world if self.ctx else 1) / 1e12  # fwd + dgrad
+        hbm = torch.cuda.max_memory_allocated(self.device) / 2 ** 30 if self.device.type == "cuda" else 0.0
+        comm = 0.0
+        if self._comm_ev is not None:
+            torch.cuda.synchronize(self.device)
+            comm = self._comm_ev[0].elapsed_time(self._comm_ev[1])
+        print(perf_line(self.rank, self.global_step, tps, tflops, hbm, comm, self.ctx.world if self.ctx else 1),
+              flush=True)
 
     # ------------------------------------------------------------------
     def save_checkpoint(self):
