@@ -6,6 +6,8 @@
 #include "ops.h"
 #include "common.h"
 
+void mift_bind_runtime(pybind11::module& m);  // runtime/loader.cpp
+
 // Device micro-step counter for graph-replayed dropout seeds (common.h mift_seed).
 static at::Tensor g_seed_step;
 const int64_t* mift_seed_step() { return g_seed_step.defined() ? g_seed_step.data_ptr<int64_t>() : nullptr; }
@@ -27,4 +29,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_seed_step", &mift_set_seed_step,
         "bind (tensor) / unbind (None) the device micro-step counter mixed into every dropout seed");
   MIFT_BIND_MORE(m);
+  mift_bind_runtime(m);
 }

@@ -159,13 +159,23 @@ def shard_indices(n: int, rank: int, world: int, mode: str = "strided", shuffle:
 class MicroBatcher:
     """Yields optimizer steps as lists of `accum` micro-batches for one rank.
 
-    Host tensors are pinned so the H2D copy is asynchronous (non_blocking)."""
+    Host tensors are pinned so the H2D copy is asynchronous (non_blocking).  With the extension
+    available the batches come from the native prefetching loader (csrc/runtime/loader.cpp:
+    a C++ worker thread gathers rows, builds masks / labels into pinned tensors ahead of the
+    consumer); ``native=False`` or ``MIFT_NATIVE_LOADER=0`` selects the Python path (same
+    batches, element for element)."""
 
     def __init__(self, ds: TokenDataset, micro_batch: int, accum: int, rank: int = 0, world: int = 1,
-                 mode: str = "strided", shuffle: bool = False, seed: int = 0, pin: bool = True):
+                 mode: str = "strided", shuffle: bool = False, seed: int = 0, pin: bool = True,
+                 native=None, prefetch: int = 4):
         self.ds, self.mb, self.accum = ds, micro_batch, accum
         self.rank, self.world, self.mode, self.shuffle, self.seed = rank, world, mode, shuffle, seed
         self.pin = pin and torch.cuda.is_available()
+        if native is None:
+            native = os.environ.get("MIFT_NATIVE_LOADER", "1") != "0"
+        self.native = bool(native) and _native_loader_available()
+        self.prefetch = prefetch
+        self._loader = None
 
     def indices(self, epoch=0):
         return shard_indices(len(self.ds), self.rank, self.world, self.mode, self.shuffle, self.seed, epoch)
@@ -178,8 +188,31 @@ class MicroBatcher:
         n = len(self.indices(0))
         return (n + self.mb - 1) // self.mb
 
+    def _native_epoch(self, idx, start_step):
+        from .. import _ext
+        if self._loader is None:
+            self._loader = _ext.require().TokenLoader(torch.from_numpy(self.ds.ids), torch.from_numpy(self.ds.lengths),
+                                                      int(self.ds.pad_id), int(self.mb), int(self.prefetch),
+                                                      bool(self.pin))
+        n_mb = (len(idx) + self.mb - 1) // self.mb
+        first = start_step * self.accum
+        self._loader.start(torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)), first)
+        step_mbs, j = [], first
+        while True:
+            item = self._loader.next()
+            if not item:
+                break
+            step_mbs.append({"input_ids": item[0], "attention_mask": item[1], "labels": item[2]})
+            j += 1
+            if len(step_mbs) == self.accum or j == n_mb:
+                yield step_mbs
+                step_mbs = []
+
     def epoch(self, epoch=0, start_step=0):
         idx = self.indices(epoch)
+        if self.native:
+            yield from self._native_epoch(idx, start_step)
+            return
         n_mb = (len(idx) + self.mb - 1) // self.mb
         step_mbs = []
         for j in range(n_mb):
@@ -192,3 +225,11 @@ class MicroBatcher:
                 if step_no >= start_step:
                     yield step_mbs
                 step_mbs = []
+
+
+def _native_loader_available():
+    try:
+        from .. import _ext
+        return _ext.available() and hasattr(_ext.require(), "TokenLoader")
+    except Exception:
+        return False
