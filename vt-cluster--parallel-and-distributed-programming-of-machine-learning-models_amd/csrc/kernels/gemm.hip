@@ -132,6 +132,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;  // 1-KiB LDS-DMA pieces per stage
   static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "stage pieces must split evenly over waves");
   constexpr int PER_STAGE = (A_INSTR + B_INSTR) / NW;  // vmcnt units per stage per wave
+  constexpr int NBUF = NSTAGE == 0 ? 2 : NSTAGE;       // NSTAGE 0 = phased schedule on 2 buffers
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (ep.sstep != nullptr) {
     ep.seed = mift_seed(ep.seed, ep.sstep);
@@ -181,13 +182,13 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
     const int nk = ke - kb;
-    // prologue: NSTAGE-1 tiles in flight
+    // prologue: NBUF-1 tiles in flight
 #pragma unroll
-    for (int s = 0; s < NSTAGE - 1; ++s)
+    for (int s = 0; s < NBUF - 1; ++s)
       if (s < nk) stage(s, (kb + s) * BK);
     for (int kt = 0; kt < nk; ++kt) {
       // tile kt landed <=> at most (#tiles issued after kt) * PER_STAGE pieces outstanding
-      if constexpr (NSTAGE >= 3) {
+      if constexpr (NBUF >= 3) {
         if (kt + 1 < nk) wait_vmcnt<PER_STAGE>();
         else wait_vmcnt<0>();
       } else {
@@ -196,8 +197,8 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // everyone's pieces of kt landed; everyone done reading kt-1
       asm volatile("" ::: "memory");  // no LDS access may move above the barrier
-      if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, (kb + kt + NSTAGE - 1) * BK);
-      const char* As = smem + (kt % NSTAGE) * STAGE_BYTES;
+      if (kt + NBUF - 1 < nk) stage((kt + NBUF - 1) % NBUF, (kb + kt + NBUF - 1) * BK);
+      const char* As = smem + (kt % NBUF) * STAGE_BYTES;
       const char* Bs = As + A_BYTES;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -219,6 +220,123 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<T>(bfv[j], af[i], acc[i][j]);
       }
     }
+  };
+
+  // ---- phased schedule (NSTAGE == 0): 256x256 tile, 2x4 waves of 128x64, BK = 64 ----
+  // Each k-tile is 4 phases, one output quadrant (64x32 of the wave tile, 16 MFMAs) each:
+  //   ph0 (q 0,0): ds_read A rows 0-63 (8) + B cols 0-31 (4)   | LDS-DMA A half 0 of tile kt+1
+  //   ph1 (q 0,1): ds_read B cols 32-63 (4)                     | LDS-DMA A half 1 of tile kt+1
+  //   ph2 (q 1,1): ds_read A rows 64-127 (8)                    |
+  //   ph3 (q 1,0): (A, B from registers)                        | LDS-DMA B halves of tile kt+2,
+  //                                                               counted vmcnt(4) retires tile kt+1
+  // phase = {reads, DMA issue, [wait]} -> s_barrier -> MFMA cluster (setprio 1) -> s_barrier.
+  // Wave row 1 (waves 4-7) runs one barrier behind row 0, so on every SIMD one wave is in its
+  // MFMA cluster while its partner issues reads / DMA (guide §5 "256² 8-phase template").
+  // Buffer hazards (two buffers, tile t in buffer t&1): a region is restaged >= 2 phases after
+  // its last ds_read (B of tile kt read last in ph1 -> B(kt+2) in ph3; A of tile kt-1 read last
+  // in its ph2 -> A(kt+1) in ph0/ph1), and read >= 1 phase after the wait that retires it.
+  auto mainloop8 = [&]() {
+   if constexpr (NSTAGE == 0) {
+    static_assert(BM == 256 && BN == 256 && NWM == 2 && NWN == 4, "phased loop: 256x256 tile, 2x4 waves");
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / BK;
+    // half h (rows 128h..128h+127) of operand o (0 = A, 1 = B) of k-tile t -> buffer t & 1
+    auto stage_half = [&](int t, int o, int h) {
+      char* base = smem + (t & 1) * STAGE_BYTES + o * A_BYTES;
+      const T* G = o ? B : A;
+      const int ld = o ? ldb : lda;
+      const int rmax = (o ? N : M) - 1;
+      const int r00 = o ? n0 : m0;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 16 * h + wave + 8 * ii;
+        const int r = i * 8 + srow;
+        const int gr = min(r00 + r, rmax);
+        __builtin_amdgcn_global_load_lds((const void*)(G + (size_t)gr * ld + t * BK + (spc ^ (r & 7)) * 8),
+                                         (void*)(base + i * 1024), 16, 0, 0);
+      }
+    };
+    const int arow = wm * WM + fr, brow = wn * WN + fr;
+    const int sw0 = (fq ^ (fr & 7)) << 4, sw1 = ((4 + fq) ^ (fr & 7)) << 4;
+    frag_t<T> af[4][2], bq[4][2];
+    auto rd = [&](const char* p) { return *reinterpret_cast<const frag_t<T>*>(p); };
+    auto cluster = [&](int qi, int qj) {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qi * 4 + i][qj * 2 + j] = mfma16<T>(bq[qj * 2 + j][kk], af[i][kk], acc[qi * 4 + i][qj * 2 + j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+
+    stage_half(0, 0, 0);
+    stage_half(0, 0, 1);
+    stage_half(0, 1, 0);
+    stage_half(0, 1, 1);
+    if (nk > 1) {
+      stage_half(1, 1, 0);
+      stage_half(1, 1, 1);
+      wait_vmcnt<4>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+    asm volatile("" ::: "memory");
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* As = smem + (kt & 1) * STAGE_BYTES;
+      const char* Bs = As + A_BYTES;
+      // ph0
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i][0] = rd(As + (arow + i * 16) * ROWB + sw0);
+        af[i][1] = rd(As + (arow + i * 16) * ROWB + sw1);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bq[j][0] = rd(Bs + (brow + j * 16) * ROWB + sw0);
+        bq[j][1] = rd(Bs + (brow + j * 16) * ROWB + sw1);
+      }
+      if (kt + 1 < nk) stage_half(kt + 1, 0, 0);
+      cluster(0, 0);
+      // ph1
+#pragma unroll
+      for (int j = 2; j < 4; ++j) {
+        bq[j][0] = rd(Bs + (brow + j * 16) * ROWB + sw0);
+        bq[j][1] = rd(Bs + (brow + j * 16) * ROWB + sw1);
+      }
+      if (kt + 1 < nk) stage_half(kt + 1, 0, 1);
+      cluster(0, 1);
+      // ph2
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i][0] = rd(As + (arow + (i + 4) * 16) * ROWB + sw0);
+        af[i][1] = rd(As + (arow + (i + 4) * 16) * ROWB + sw1);
+      }
+      cluster(1, 1);
+      // ph3
+      if (kt + 2 < nk) {
+        stage_half(kt + 2, 1, 0);
+        stage_half(kt + 2, 1, 1);
+        wait_vmcnt<4>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      cluster(1, 0);
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();  // re-align the rows (equal barrier counts)
+   }
   };
 
   // fused epilogue of the (m0, n0) tile from acc (+ LoRA K-extension)
@@ -353,7 +471,8 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     }
     m0 = (bid / ntn) * BM;
     n0 = (bid % ntn) * BN;
-    mainloop(0, nk_all);
+    if constexpr (NSTAGE == 0) mainloop8();
+    else mainloop(0, nk_all);
     epilogue();
     return;
   } else {
@@ -430,7 +549,7 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
                  int K, const EpiArgs& ep, hipStream_t st) {
   constexpr int STAGE_BYTES = (BM + BN) * ROWB;
   constexpr int EPI_BYTES = BM * (BN + 8) * 2;
-  constexpr int RING = NSTAGE * STAGE_BYTES;
+  constexpr int RING = (NSTAGE == 0 ? 2 : NSTAGE) * STAGE_BYTES;
   constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
   constexpr int NT = NWM * NWN * 64;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
@@ -494,20 +613,24 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
 //   6: 128x256, 8 waves (2x4), 2-stage ring (96 KiB)
 //   7: 128x96,  4 waves (2x2, wave tile 64x48), 2-stage ring (56 KiB, 2 blocks/CU) — balances
 //      ragged waves: N=768 gives 512 tiles = exactly one wave of 2x256 slots (128x128: 384)
+//   8: 256x256, 8 waves (2x4), phased schedule (mainloop8: 4 phases per k-tile, staggered wave
+//      rows, counted vmcnt across barriers, setprio MFMA clusters)
 template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
   if (tile == 0) {
     // auto, from tools/bench_kernels.py on MI355X (profiles/bench_gemm_tiles_sk.json):
-    //  * 256x256 (tile 5) wins whenever there are enough big tiles and K is not tiny
-    //    (OPT-2.7B qkv/out/fc1 fwd, fc2 dgrad, LM heads: +5..30 % over 128x128);
-    //  * long-K problems with few 256x256 tiles (N = 2560, K >= 4096: fc2 fwd, qkv/fc1 dgrad)
-    //    run 128x256 + the split-K ragged-wave tail (+15..30 %);
-    //  * distilgpt2-scale problems (K = 768..3072, N <= 3072) keep the 128x128 tile.
+    //  * the phased 256x256 kernel (tile 8) wins with >= half a chip-wave of 256x256 tiles at
+    //    K >= 1024 (OPT-2.7B every GEMM at M = 4096: +10..30 % over tiles 5/6 in isolation,
+    //    profiles/bench_gemm_p8.json) or with very many tiles;
+    //  * long-K problems with few 256x256 tiles (M = 2048, N = 2560, K >= 4096) run 128x256 +
+    //    the split-K ragged-wave tail;
+    //  * distilgpt2-scale problems (K = 768, N <= 3072) keep 128x128 / 128x96: at 1.1-1.5 waves of
+    //    256x256 tiles with a gelu/pre-activation epilogue tile 8 ran 10-20 % slower end to end.
     const long n256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-    if (K >= 4096 && n256 < 256 && t128 >= 128) tile = 6;
-    else if ((K >= 1024 && n256 >= 128) || n256 >= 2048) tile = 5;
+    if ((K >= 1024 && n256 >= 128) || n256 >= 2048) tile = 8;
+    else if (K >= 4096 && t128 >= 128) tile = 6;
     else if (t128 >= 64) {
       tile = 3;
       // 128x96 when its whole-wave count x tile area beats 128x128's (5 % per-tile
@@ -526,6 +649,7 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     case 5: launch_gemm<T, 256, 256, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 6: launch_gemm<T, 128, 256, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 7: launch_gemm<T, 128, 96, 2, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 8: launch_gemm<T, 256, 256, 2, 4, 0>(a, b, c, a2, b2, M, N, K, ep, st); break;
     default: launch_gemm<T, 64, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
   }
 }

@@ -247,10 +247,14 @@ class MLP(torch.autograd.Function):
     def forward(ctx, h, ln_w, ln_b, fc1, fc2, eps, act, p, seed, seed_l1, seed_l2, training, n1, *lparams):
         shp = h.shape
         h2 = _flat(h.contiguous())
-        a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
         lo1 = fc1.lora_ops(h.dtype) if n1 else None
         lo2 = fc2.lora_ops(h.dtype) if len(lparams) > n1 else None
-        T1 = lo1.forward(a, seed_l1, training) if lo1 is not None else None
+        if lo1 is not None:  # LN and fc1's LoRA input projection in one row pass (OPT targets fc1)
+            a, mean, rstd, T1 = K.layer_norm_fwd_proj(h2, ln_w, ln_b, eps, lo1.A32s, lo1.rows, 1.0,
+                                                      lo1.p if training else 0.0, seed_l1)
+        else:
+            a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
+            T1 = None
         f, z = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, want_preact=True)
         T2 = lo2.forward(f, seed_l2, training) if lo2 is not None else None
         pp = p if training else 0.0
