@@ -75,6 +75,45 @@ def bench_gemm(results, shapes=None, dtype=torch.bfloat16):
         results.append(row)
 
 
+# distilgpt2 GEMMs with the epilogues they run with in training (fused block Functions)
+DGPT_CASES = [
+    # name, M, N, K, epilogue kwargs
+    ("c_attn.fwd+ext+bias", 8192, 2304, 768, dict(bias=1, ext=1)),
+    ("attn.c_proj.fwd+ext+drop+res", 8192, 768, 768, dict(bias=1, ext=1, p=0.1, res=1)),
+    ("c_fc.fwd+gelu+preact", 8192, 3072, 768, dict(bias=1, act=1, pre=1)),
+    ("mlp.c_proj.fwd+ext+drop+res", 8192, 768, 3072, dict(bias=1, ext=1, p=0.1, res=1)),
+    ("c_attn.dgrad+maskext", 8192, 768, 2304, dict(ext=1, ext_p=0.05)),
+    ("c_fc.dgrad", 8192, 768, 3072, dict()),
+    ("mlp.c_proj.dgrad+maskext+gelubwd", 8192, 3072, 768, dict(ext=1, ext_p=0.05, act=4, aux=1)),
+    ("attn.c_proj.dgrad+maskext", 8192, 768, 768, dict(ext=1, ext_p=0.05)),
+]
+
+
+def bench_dgpt(results):
+    import mift._C as C
+    dt = torch.bfloat16
+    tot = {}
+    for name, M, N, K, e in DGPT_CASES:
+        a = torch.randn(M, K, device="cuda", dtype=dt)
+        b = torch.randn(N, K, device="cuda", dtype=dt) / K ** 0.5
+        bias = torch.randn(N, device="cuda", dtype=dt) if e.get("bias") else None
+        a2 = torch.randn(M, 32, device="cuda", dtype=dt) if e.get("ext") else None
+        b2 = torch.randn(N, 32, device="cuda", dtype=dt) if e.get("ext") else None
+        aux = torch.randn(M, N, device="cuda", dtype=dt) if e.get("aux") else None
+        res = torch.randn(M, N, device="cuda", dtype=dt) if e.get("res") else None
+        fl = 2.0 * M * N * K
+        row = {"name": name, "M": M, "N": N, "K": K}
+        for tile in TILES:
+            t = timeit(lambda: C.gemm_nt(a, b, bias, a2, b2, e.get("act", 0), aux, res, e.get("p", 0.0), 3,
+                                         bool(e.get("pre", 0)), 1.0, None, tile, None, None, e.get("ext_p", 0.0), 7))
+            row[f"mift_t{tile}_us"] = round(t * 1e3, 1)
+            row[f"mift_t{tile}_tflops"] = round(fl / t / 1e9, 1)
+            tot[tile] = tot.get(tile, 0.0) + t * 1e3
+        print(json.dumps(row), flush=True)
+        results.append(row)
+    print("per-layer total us by tile:", json.dumps({k: round(v, 1) for k, v in tot.items()}), flush=True)
+
+
 def bench_ln(results):
     import mift._C as C
     for M, D in [(8192, 768), (2048, 2560), (8192, 4096)]:
@@ -98,7 +137,7 @@ def main():
     assert mift.kernels_available(), mift._ext.error()
     results = []
     for k in a.only.split(","):
-        {"gemm": bench_gemm, "ln": bench_ln,
+        {"gemm": bench_gemm, "ln": bench_ln, "dgpt": bench_dgpt,
          "opt": lambda r: bench_gemm(r, OPT_SHAPES, torch.float16)}[k](results)
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)

@@ -255,7 +255,11 @@ class MLP(torch.autograd.Function):
         else:
             a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
             T1 = None
-        f, z = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, want_preact=True)
+        if act == 2:  # ReLU: relu'(z) = [f > 0], so f doubles as the backward's aux (no pre-activation store)
+            f = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act)
+            z = f
+        else:
+            f, z = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, want_preact=True)
         T2 = lo2.forward(f, seed_l2, training) if lo2 is not None else None
         pp = p if training else 0.0
         out = K.gemm(f, fc2.w_nk(), fc2.bias, T2, lo2.B32 if lo2 else None, residual=h2, dropout_p=pp, seed=seed)
