@@ -89,6 +89,40 @@ DGPT_CASES = [
 ]
 
 
+OPT_CASES = [  # OPT-2.7B at micro-batch 48 x 512 tokens, fp16
+    ("opt.out.fwd+ext+drop+res", 24576, 2560, 2560, dict(bias=1, ext=1, p=0.1, res=1)),
+    ("opt.fc1.fwd+ext+relu", 24576, 10240, 2560, dict(bias=1, ext=1, act=2)),
+    ("opt.fc2.fwd+ext+drop+res", 24576, 2560, 10240, dict(bias=1, ext=1, p=0.1, res=1)),
+    ("opt.fc2.dgrad+maskext+relubwd", 24576, 10240, 2560, dict(ext=1, ext_p=0.05, act=5, aux=1)),
+    ("opt.qkv.dgrad+maskext", 24576, 2560, 7680, dict(ext=1, ext_p=0.05)),
+]
+
+
+def bench_epi_ab(results):
+    """Epilogue prefetch A/B (MIFT_EPI_PREFETCH 0 vs 1) interleaved in one process (guide rule 24)."""
+    import mift._C as C
+    for name, M, N, K, e in DGPT_CASES + OPT_CASES:
+        dt = torch.float16 if name.startswith("opt") else torch.bfloat16
+        a = torch.randn(M, K, device="cuda", dtype=dt)
+        b = torch.randn(N, K, device="cuda", dtype=dt) / K ** 0.5
+        bias = torch.randn(N, device="cuda", dtype=dt) if e.get("bias") else None
+        a2 = torch.randn(M, 32, device="cuda", dtype=dt) if e.get("ext") else None
+        b2 = torch.randn(N, 32, device="cuda", dtype=dt) if e.get("ext") else None
+        aux = torch.randn(M, N, device="cuda", dtype=dt) if e.get("aux") else None
+        res = torch.randn(M, N, device="cuda", dtype=dt) if e.get("res") else None
+        fn = lambda: C.gemm_nt(a, b, bias, a2, b2, e.get("act", 0), aux, res, e.get("p", 0.0), 3,  # noqa: E731
+                               bool(e.get("pre", 0)), 1.0, None, 0, None, None, e.get("ext_p", 0.0), 7)
+        ts = {0: [], 1: []}
+        for _ in range(3):
+            for pf in (0, 1):
+                os.environ["MIFT_EPI_PREFETCH"] = str(pf)
+                ts[pf].append(timeit(fn, rounds=3))
+        os.environ.pop("MIFT_EPI_PREFETCH", None)
+        row = {"name": name, "pf0_us": round(min(ts[0]) * 1e3, 1), "pf1_us": round(min(ts[1]) * 1e3, 1)}
+        print(json.dumps(row), flush=True)
+        results.append(row)
+
+
 def bench_dgpt(results):
     import mift._C as C
     dt = torch.bfloat16
@@ -137,7 +171,7 @@ def main():
     assert mift.kernels_available(), mift._ext.error()
     results = []
     for k in a.only.split(","):
-        {"gemm": bench_gemm, "ln": bench_ln, "dgpt": bench_dgpt,
+        {"gemm": bench_gemm, "ln": bench_ln, "dgpt": bench_dgpt, "epi": bench_epi_ab,
          "opt": lambda r: bench_gemm(r, OPT_SHAPES, torch.float16)}[k](results)
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)

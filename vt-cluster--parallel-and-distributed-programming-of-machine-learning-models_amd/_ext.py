@@ -21,11 +21,13 @@ def _load():
     if _C is not None or _ERR is not None:
         return
     here = os.path.dirname(os.path.abspath(__file__))
-    so = None
-    for f in os.listdir(here):
-        if f.startswith("_C") and f.endswith(".so"):
-            so = os.path.join(here, f)
-            break
+    so = os.environ.get("MIFT_EXT_SO")  # explicit build (A/B runs of two builds on one device)
+    if not so:
+        cands = sorted(f for f in os.listdir(here) if f.startswith("_C") and f.endswith(".so"))
+        if "_C.so" in cands:
+            cands.remove("_C.so")
+            cands.insert(0, "_C.so")
+        so = os.path.join(here, cands[0]) if cands else None
     if so is None:
         _ERR = ImportError(f"mift extension not built (no _C*.so in {here}); run `python -m mift.build`")
         return

@@ -165,6 +165,18 @@ MIFT_HD float block_sum(float v, float* scratch) {
   return r;
 }
 
+// 8 packed 16-bit elements -> fp32
+template <typename T>
+MIFT_HD void unpack8(short8 v, float* out) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    short s = v[i];
+    T t;
+    __builtin_memcpy(&t, &s, 2);
+    out[i] = (float)t;
+  }
+}
+
 // Vector load/store of 8 elements (16 B per lane for 16-bit types, Guideline 13).
 template <typename T>
 MIFT_HD void load8(const T* p, float* out) {

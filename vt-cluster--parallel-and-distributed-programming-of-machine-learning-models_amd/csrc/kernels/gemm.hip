@@ -68,6 +68,7 @@ struct EpiArgs {
   uint64_t ext_seed;
   float ext_inv_keep;
   const int64_t* sstep;    // device micro-step for graph-replayed dropout seeds (common.h mift_seed)
+  int prefetch;            // epilogue: load aux / residual of all chunks up front (MIFT_EPI_PREFETCH=1; opt-in)
 };
 
 // Split-K tail (second launch of a hybrid data-parallel + split-K GEMM): the
@@ -400,11 +401,35 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     __syncthreads();
 
     // ---- epilogue phase 2: 8 columns per thread, 16-B vector I/O, whole rows ----
+    // The global operands of ALL this thread's chunks (activation aux, residual) are loaded up
+    // front (acc is dead here), so their HBM latency is paid once per tile rather than once per
+    // chunk behind the previous chunk's store; loads are unconditional from clamped addresses
+    // (no per-chunk branch around a load: guide §5 "Projection GEMM" item 4(c)).
     constexpr int VPR = BN / 8;
-    for (int v = tid; v < BM * VPR; v += NT) {
+    constexpr int ITER = BM * VPR / NT;
+    static_assert((BM * VPR) % NT == 0, "epilogue chunks must split evenly over the threads");
+    // Measured: -2..8 % per GEMM in isolation on the 128x96 / 128x128 tiles but +1.5 % on the
+    // distilgpt2 step (same-device A/B), +2..5 % slower on the 256x256 tile (16 chunks per thread
+    // per operand burst at once): opt-in (MIFT_EPI_PREFETCH=1), small tiles only.  The default
+    // loop stays rolled: unrolling it with the generic activation switch cost the 256x256 ReLU
+    // epilogues 20 % (OPT fc1 fwd 1395 -> 1121 us, fc2 dgrad 1594 -> 1321 us at M = 24576).
+    constexpr bool PF_OK = ITER <= 8;
+    const bool pf_aux = PF_OK && ep.prefetch && ep.aux != nullptr && ep.act != ACT_NONE && N >= 8;
+    const bool pf_res = PF_OK && ep.prefetch && ep.residual != nullptr && N >= 8;
+    auto prefetch = [&](const void* src, short8* dst) {
+  #pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int v = tid + it * NT;
+        const int gr = min(m0 + v / VPR, M - 1), gc = min(n0 + (v % VPR) * 8, N - 8);
+        dst[it] = *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(src) + (size_t)gr * ldc + gc);
+      }
+    };
+    // one 8-column chunk: (aux, res) come prefetched when have_aux / have_res
+    auto chunk = [&](int it, bool have_aux, short8 auxv, bool have_res, short8 resv) {
+      const int v = tid + it * NT;
       const int row = v / VPR, c8 = (v % VPR) * 8;
       const int gr = m0 + row, gc = n0 + c8;
-      if (gr >= M || gc >= N) continue;
+      if (gr >= M || gc >= N) return;
       float z[8];
       load8<T>(Cs + row * CLD + c8, z);
       const size_t off = (size_t)gr * ldc + gc;
@@ -423,7 +448,8 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       if (ep.act != ACT_NONE) {
         float ax[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (ep.aux != nullptr) {
-          if (full) load8<T>(reinterpret_cast<const T*>(ep.aux) + off, ax);
+          if (full && have_aux) unpack8<T>(auxv, ax);
+          else if (full) load8<T>(reinterpret_cast<const T*>(ep.aux) + off, ax);
           else for (int e = 0; e < N - gc; ++e) ax[e] = (float)reinterpret_cast<const T*>(ep.aux)[off + e];
         }
         // one uniform branch per 8 elements (not a switch per element)
@@ -435,6 +461,14 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
           case ACT_GELU_TANH_BWD:
   #pragma unroll
             for (int e = 0; e < 8; ++e) z[e] *= gelu_tanh_grad(ax[e]);
+            break;
+          case ACT_RELU:
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) z[e] = fmaxf(z[e], 0.f);
+            break;
+          case ACT_RELU_BWD:
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) z[e] = ax[e] > 0.f ? z[e] : 0.f;
             break;
           default:
   #pragma unroll
@@ -449,13 +483,27 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       }
       if (ep.residual != nullptr) {
         float rv[8];
-        if (full) load8<T>(reinterpret_cast<const T*>(ep.residual) + off, rv);
+        if (full && have_res) unpack8<T>(resv, rv);
+        else if (full) load8<T>(reinterpret_cast<const T*>(ep.residual) + off, rv);
         else for (int e = 0; e < N - gc; ++e) rv[e] = (float)reinterpret_cast<const T*>(ep.residual)[off + e];
   #pragma unroll
         for (int e = 0; e < 8; ++e) z[e] += rv[e];
       }
       if (full) store8<T>(C + off, z);
       else for (int e = 0; e < N - gc; ++e) C[off + e] = (T)z[e];
+    };
+    if constexpr (PF_OK) {
+      if (!ep.prefetch) {
+        for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{});
+        return;
+      }
+      short8 aux_r[ITER], res_r[ITER];
+      if (pf_aux) prefetch(ep.aux, aux_r);
+      if (pf_res) prefetch(ep.residual, res_r);
+  #pragma unroll
+      for (int it = 0; it < ITER; ++it) chunk(it, pf_aux, aux_r[it], pf_res, res_r[it]);
+    } else {
+      for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{});
     }
   };
 
@@ -720,6 +768,10 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
   ep.ext_seed = (uint64_t)ext_seed;
   ep.ext_inv_keep = ext_p > 0 ? mift_inv_keep(ext_p) : 1.f;
   ep.sstep = mift_seed_step();
+  {
+    const char* e = getenv("MIFT_EPI_PREFETCH");  // read per call: A/B-able within one process
+    ep.prefetch = e ? atoi(e) : 0;
+  }
   ep.pre_add = nullptr;
   if (pre_add) {
     TORCH_CHECK(pre_add->size(0) == M && pre_add->size(1) == N && pre_add->stride(0) == c.stride(0) &&
