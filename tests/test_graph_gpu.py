@@ -3,7 +3,8 @@
 Same seeds, same data: graph replay must draw the same dropout masks (device
 micro-step counter, csrc/common.h mift_seed) and produce the same losses and
 LoRA parameters as eager execution, step after step (tolerance only for the
-fp32 atomic accumulation order of the LoRA weight-gradient kernels)."""
+fp32 atomic accumulation order of the LoRA weight-gradient kernels, which Adam
+amplifies to +-lr on gradients that are zero up to rounding)."""
 import pytest
 import torch
 
@@ -47,15 +48,20 @@ def _run(graph, model_name, steps=5, mb=4, accum=2, S=128, precision="bf16"):
 def test_graph_replay_matches_eager(name, precision):
     assert mift.kernels_available()
     le, pe, _ = _run(False, name, precision=precision)
-    _, pe2, _ = _run(False, name, precision=precision)
     lg, pg, tr = _run(True, name, precision=precision)
-    # eager itself is not bit-reproducible (fp32 atomics in the LoRA wgrad kernels, amplified by
-    # Adam on near-zero gradients): the graph must stay within that run-to-run noise
-    noise = (pe - pe2).abs().max().item()
     assert tr.graphed is not None and len(tr.graphed.graphs) == 1, "graph was not captured"
     assert le[0] == pytest.approx(lg[0], rel=1e-6, abs=1e-6)  # step 1 is the eager warm-up in both
     for a, b in zip(le, lg):
-        assert a == pytest.approx(b, rel=2e-3, abs=2e-3), (le, lg)
-    err = (pe - pg).abs().max().item()
-    assert err <= 3 * noise + 2e-4, (err, noise)
+        assert a == pytest.approx(b, rel=1e-4, abs=1e-4), (le, lg)
+    # Neither path is bit-reproducible: the LoRA weight-gradient kernels accumulate with fp32
+    # atomics, and Adam's first steps move every element by ~lr * sign(g), so a gradient that is
+    # ~0 up to rounding can flip sign between runs and shift that element by up to 2*lr per step
+    # (measured on MI355X: eager-vs-eager and graph-vs-graph both reach ~0.93*lr).  A real replay
+    # bug (stale inputs, repeated masks, stale LoRA operands) moves the bulk of the parameters and
+    # the losses instead, so bound the fraction of disagreeing elements and the losses.
+    lr = 1e-3
+    d = (pe - pg).abs()
+    frac = (d > 0.2 * lr).float().mean().item()
+    assert d.max().item() <= 2 * lr * 5 + 1e-6, d.max().item()
+    assert frac < 0.01, frac
     assert len(set(round(x, 6) for x in lg)) == len(lg), "replays must not repeat masks/losses"

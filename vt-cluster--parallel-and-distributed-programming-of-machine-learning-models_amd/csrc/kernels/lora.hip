@@ -328,8 +328,11 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
     ws = wsb.data_ptr<float>();
   }
   const int grid = mblocks * KS;
-  // 8 waves per row block when each of 4 waves would walk > 8 k-steps (K/KS > 1024)
-  const bool wide = nks / KS > 32;
+  // 4 waves per row block (MIFT_LORA_NW=8 for 8): the 8-wave variant for long K measured slower
+  // at OPT-2.7B shapes (M = 24576: K = 2560 35.6 vs 30.3 us, K = 7680 118 vs 105, K = 10240 155 vs
+  // 140; tools/bench_rowproj.py) and even at distilgpt2's
+  static const int nw_env = [] { const char* e = getenv("MIFT_LORA_NW"); return e ? atoi(e) : 4; }();
+  const bool wide = nw_env == 8;
   auto go = [&](auto tt) {
     using T = decltype(tt);
     if (wide)

@@ -23,10 +23,38 @@ Any projection object passed as ``lin`` provides ``w_nk()``, ``w_kn()``,
 adapter-operand object (``AdapterOps`` for one adapter, or the multi-adapter
 variant used by OPT's fused q/k/v projection — mift.models.opt).
 """
+import os
+
 import torch
 
 from . import kernels as K
 from .streams import run_side
+
+# LN fused with the LoRA input projection does LR FMAs per element on the VALU with the [LR,D]
+# operand re-read from cache for every row: a win for one adapter (LR = 8), but for OPT's fused
+# q/k/v adapters (24 rows -> LR = 32) it ran 475 us at M = 24576, D = 2560 against LN + the MFMA
+# lora_proj (tools/bench_rowproj.py) — above this many rows, LN and projection run separately.
+# One adapter at OPT's D = 2560 lost too (125 us vs 46 + 40 us); at distilgpt2's D = 768 it is even
+# (17.2 vs 7.6 + 8.9 us) and saves a launch.
+_LNPROJ_MAX_ROWS = int(os.environ.get("MIFT_LNPROJ_MAX_ROWS", "8"))
+_LNPROJ_MAX_D = int(os.environ.get("MIFT_LNPROJ_MAX_D", "1024"))
+
+
+def _ln_fwd_lora(x2, ln_w, ln_b, eps, lo, seed, training):
+    """(LN(x), mean, rstd, T32 = s·dropout(LN(x))·Aᵀ) — fused row pass or LN + lora_proj."""
+    if lo.rows <= _LNPROJ_MAX_ROWS and x2.shape[-1] <= _LNPROJ_MAX_D:
+        return K.layer_norm_fwd_proj(x2, ln_w, ln_b, eps, lo.A32s, lo.rows, 1.0, lo.p if training else 0.0, seed)
+    a, mean, rstd = K.layer_norm_fwd(x2, ln_w, ln_b, eps)
+    return a, mean, rstd, lo.forward(a, seed, training)
+
+
+def _mask_proj(g2, p, seed, lo):
+    """(gz = dropout-bwd(g), dT0 = dt_alpha·gz·B) — one row pass at small D; at OPT's D = 2560 the
+    row pass (79 us) lost to mask_scale + the hipBLASLt projection (38 + 22 us)."""
+    if lo.rows <= _LNPROJ_MAX_ROWS and g2.shape[-1] <= _LNPROJ_MAX_D:
+        return K.mask_proj(g2, p, seed, lo.B32t, lo.rows, lo.dt_alpha)
+    gz = K.mask_scale(g2, p, seed) if p > 0 else g2
+    return gz, K.lora_proj(gz, lo.B32t, lo.dt_alpha, 0.0, 0)
 
 _BWD = {0: 0, 1: 4, 2: 5, 3: 6}
 
@@ -179,8 +207,7 @@ class LnLinear(torch.autograd.Function):
         x2 = _flat(x.contiguous())
         lo = lin.lora_ops(x.dtype) if lparams else None
         if lo is not None:  # LN and the LoRA input projection in one row pass (csrc/kernels/rowproj.hip)
-            a, mean, rstd, T32 = K.layer_norm_fwd_proj(x2, ln_w, ln_b, eps, lo.A32s, lo.rows, 1.0,
-                                                       lo.p if training else 0.0, lora_seed)
+            a, mean, rstd, T32 = _ln_fwd_lora(x2, ln_w, ln_b, eps, lo, lora_seed, training)
         else:
             a, mean, rstd = K.layer_norm_fwd(x2, ln_w, ln_b, eps)
             T32 = None
@@ -226,7 +253,7 @@ class LinearResidual(torch.autograd.Function):
         lin, lo = ctx.lin, ctx.lo
         gh2 = _flat(gh.contiguous())
         if lo is not None:  # residual-dropout backward and dT = s·gz·B in one row pass
-            gz, dT0 = K.mask_proj(gh2, ctx.p, ctx.seed, lo.B32t, lo.rows, lo.dt_alpha)
+            gz, dT0 = _mask_proj(gh2, ctx.p, ctx.seed, lo)
             lg, dT32 = lo.backward(gz, x2, T32, ctx.lseed, ctx.training, dT32=dT0)
         else:
             gz = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
@@ -250,8 +277,7 @@ class MLP(torch.autograd.Function):
         lo1 = fc1.lora_ops(h.dtype) if n1 else None
         lo2 = fc2.lora_ops(h.dtype) if len(lparams) > n1 else None
         if lo1 is not None:  # LN and fc1's LoRA input projection in one row pass (OPT targets fc1)
-            a, mean, rstd, T1 = K.layer_norm_fwd_proj(h2, ln_w, ln_b, eps, lo1.A32s, lo1.rows, 1.0,
-                                                      lo1.p if training else 0.0, seed_l1)
+            a, mean, rstd, T1 = _ln_fwd_lora(h2, ln_w, ln_b, eps, lo1, seed_l1, training)
         else:
             a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
             T1 = None
@@ -277,7 +303,7 @@ class MLP(torch.autograd.Function):
         lg1, lg2 = _nones(ctx.n1), _nones(ctx.n2)
         dT1 = dT2 = None
         if lo2 is not None:  # residual-dropout backward fused with dT2 = s·gm·B2
-            gm, dT0 = K.mask_proj(gh2, ctx.p, ctx.seed, lo2.B32t, lo2.rows, lo2.dt_alpha)
+            gm, dT0 = _mask_proj(gh2, ctx.p, ctx.seed, lo2)
             lg2, dT2 = lo2.backward(gm, f, T2, ctx.sl2, ctx.training, dT32=dT0)
         else:
             gm = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
