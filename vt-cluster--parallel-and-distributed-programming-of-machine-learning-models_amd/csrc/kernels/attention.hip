@@ -147,19 +147,28 @@ MIFT_HD bool drop_keep(uint64_t seed, uint32_t thr, int64_t bh, int S, int q, in
 }
 
 // ============================== forward ====================================
-template <typename T, int HD>
+// QG query groups of 16 per wave (block = 64·QG queries): every K fragment
+// (ds_read_b128) and V^T fragment (two ds_read_b64_tr_b16) read from LDS feeds
+// QG MFMAs instead of one.  With QG = 1 a 16x16x32 MFMA (8 cycles on its
+// SIMD) needs 1 KiB of LDS reads (8 cycles of the CU's shared 128 B/clk LDS
+// port), so four waves are LDS-bound 4:1; QG = 2 halves the LDS bytes per
+// MFMA and the K/V global->LDS traffic per query.  Groups whose 16 queries all
+// precede a key tile skip it (wave-uniform branch; same result as a fully
+// masked tile).
+template <typename T, int HD, int QG>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ kv_len,
                                                        int B, int S, int H, float scale, uint64_t seed,
                                                        const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
+  constexpr int BQB = BQ * QG;  // queries per block
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;                    // [64][HDP] b128 image
   char* Vs = smem + G::ROW_BYTES;     // [64][HD] tr image
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, qc = lane & 15;
-  const int nqt = (S + BQ - 1) / BQ;
+  const int nqt = (S + BQB - 1) / BQB;
   const int qt = nqt - 1 - (blockIdx.x % nqt);  // heavy (late) query tiles first
   const int bh = blockIdx.x / nqt;
   const int b = bh / H, h = bh % H;
@@ -169,22 +178,27 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
   const T* Kg = Qg + D;
   const T* Vg = Qg + 2 * D;
   const int klen = kv_len ? kv_len[b] : S;
-  const int q0 = qt * BQ + wave * 16;
-  const int myq = q0 + qc;
+  const int q0 = qt * BQB + wave * 16 * QG;  // first query of this wave; group j: q0 + 16 j
   const float c2 = scale * LOG2E;
   const bool hz = (uint64_t)B * H * S * S < (1ull << 33);  // dropout pairs' high word is 0: hoisted hash
   const uint32_t hm0 = mift_hmix(seed, 0);
 
-  vec8<T> qf[G::NKS];
-  load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
+  vec8<T> qf[QG][G::NKS];
+#pragma unroll
+  for (int j = 0; j < QG; ++j) load_reg_frags<T, HD>(qf[j], Qg, ld, q0 + 16 * j + qc, S, lane);
   zero_row_pad<HD>(Ks, tid);
 
-  float m = -INFINITY, l = 0.f;
-  float4_ o[G::NOT];
+  float m[QG], l[QG];
+  float4_ o[QG][G::NOT];
 #pragma unroll
-  for (int i = 0; i < G::NOT; ++i) o[i] = float4_{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < QG; ++j) {
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < G::NOT; ++i) o[j][i] = float4_{0.f, 0.f, 0.f, 0.f};
+  }
 
-  const int kend = min((qt + 1) * BQ, klen);
+  const int kend = min((qt + 1) * BQB, klen);
   const int nkt = (kend + BKV - 1) / BKV;
   TileRegs<HD> kr, vr;
   if (nkt > 0) {
@@ -201,84 +215,108 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
       kr.load(Kg, ld, k0 + BKV, S, tid);
       vr.load(Vg, ld, k0 + BKV, S, tid);
     }
-    float4_ st[4];
+    bool act[QG];
+#pragma unroll
+    for (int j = 0; j < QG; ++j) act[j] = k0 <= q0 + 16 * j + 15;
+    if (!act[0]) continue;  // groups are in query order: none of this wave's queries sees the tile
+    float4_ st[QG][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      st[t] = float4_{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < G::NKS; ++s)
-        st[t] = mfma16(ld_frag<T>(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], st[t]);
+      for (int j = 0; j < QG; ++j) st[j][t] = float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < G::NKS; ++s) {
+        const vec8<T> kf = ld_frag<T>(Ks + (t * 16 + qc) * G::RS + (4 * s + g) * 16);
+#pragma unroll
+        for (int j = 0; j < QG; ++j)
+          if (act[j]) st[j][t] = mfma16(kf, qf[j][s], st[j][t]);
+      }
     }
-    const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
-    float tmax = -INFINITY;
+    vec8<T> pf[QG][2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int j = 0; j < QG; ++j) {
+      if (!act[j]) continue;
+      const int q0j = q0 + 16 * j, myq = q0j + qc;
+      const bool diag = (k0 + BKV > q0j) || (k0 + BKV > klen);
+      float tmax = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = st[t][r] * c2;
-        if (diag) {
-          const int key = k0 + t * 16 + g * 4 + r;
-          if (key > myq || key >= klen) v = -INFINITY;
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = st[j][t][r] * c2;
+          if (diag) {
+            const int key = k0 + t * 16 + g * 4 + r;
+            if (key > myq || key >= klen) v = -INFINITY;
+          }
+          st[j][t][r] = v;
+          tmax = fmaxf(tmax, v);
         }
-        st[t][r] = v;
-        tmax = fmaxf(tmax, v);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      // lazy rescale: the running max only moves when some row's tile max exceeds it by
+      // > 2^8 (p <= 256 stays exact in fp32 and representable in bf16/fp16), so most tiles
+      // skip the O rescale and its accumulator round trips (wave-uniform branch)
+      const bool resc = __any(tmax > m[j] + 8.f);
+      float alpha = 1.f;
+      if (resc) {
+        const float mnew = fmaxf(m[j], tmax);
+        alpha = (m[j] == -INFINITY) ? 0.f : fast_exp2(m[j] - mnew);
+        m[j] = mnew;
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    // lazy rescale: the running max only moves when some row's tile max exceeds it by
-    // > 2^8 (p <= 256 stays exact in fp32 and representable in bf16/fp16), so most tiles
-    // skip the O rescale and its accumulator round trips (wave-uniform branch)
-    const bool resc = __any(tmax > m + 8.f);
-    float alpha = 1.f;
-    if (resc) {
-      const float mnew = fmaxf(m, tmax);
-      alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mnew);
-      m = mnew;
-    }
-    float psum = 0.f;
-    vec8<T> pf[2];
+      float psum = 0.f;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      bool kp[4] = {true, true, true, true};
-      if (thr != 0) {
-        const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
-        if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
-        else mift_keep4(seed, i0, thr, kp);
+      for (int t = 0; t < 4; ++t) {
+        bool kp[4] = {true, true, true, true};
+        if (thr != 0) {
+          const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
+          if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
+          else mift_keep4(seed, i0, thr, kp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = (m[j] == -INFINITY) ? 0.f : fast_exp2(st[j][t][r] - m[j]);
+          psum += p;
+          if (thr != 0) p = kp[r] ? p * inv_keep : 0.f;
+          pf[j][t >> 1][(t & 1) * 4 + r] = (T)p;
+        }
       }
+      l[j] = l[j] * alpha + psum;
+      if (resc) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float p = (m == -INFINITY) ? 0.f : fast_exp2(st[t][r] - m);
-        psum += p;
-        if (thr != 0) p = kp[r] ? p * inv_keep : 0.f;
-        pf[t >> 1][(t & 1) * 4 + r] = (T)p;
-      }
-    }
-    l = l * alpha + psum;
-    if (resc) {
+        for (int r = 0; r < 4; ++r) {
+          const float ar = __shfl(alpha, g * 4 + r, 64);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ar = __shfl(alpha, g * 4 + r, 64);
-#pragma unroll
-        for (int i = 0; i < G::NOT; ++i) o[i][r] *= ar;
+          for (int i = 0; i < G::NOT; ++i) o[j][i][r] *= ar;
+        }
       }
     }
 #pragma unroll
     for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) o[i] = mfma16(pf[s2], tr_frag<T>(Vs, G::TRS, 32 * s2, i * 16, lane), o[i]);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const vec8<T> vf = tr_frag<T>(Vs, G::TRS, 32 * s2, i * 16, lane);
+#pragma unroll
+        for (int j = 0; j < QG; ++j)
+          if (act[j]) o[j][i] = mfma16(pf[j][s2], vf, o[j][i]);
+      }
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  const float inv_l = l > 0.f ? 1.f / l : 0.f;
-  if (g == 0 && myq < S) lse[(int64_t)bh * S + myq] = (l > 0.f) ? (m + log2f(l)) * LN2 : -INFINITY;
   T* Og = out + (int64_t)b * S * D + h * HD;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float il = __shfl(inv_l, g * 4 + r, 64);
-    const int q = q0 + g * 4 + r;
-    if (q < S) {
+  for (int j = 0; j < QG; ++j) {
+    float lj = l[j];
+    lj += __shfl_xor(lj, 16, 64);
+    lj += __shfl_xor(lj, 32, 64);
+    const float inv_l = lj > 0.f ? 1.f / lj : 0.f;
+    const int q0j = q0 + 16 * j, myq = q0j + qc;
+    if (g == 0 && myq < S) lse[(int64_t)bh * S + myq] = (lj > 0.f) ? (m[j] + log2f(lj)) * LN2 : -INFINITY;
 #pragma unroll
-      for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (T)(o[i][r] * il);
+    for (int r = 0; r < 4; ++r) {
+      const float il = __shfl(inv_l, g * 4 + r, 64);
+      const int q = q0j + g * 4 + r;
+      if (q < S) {
+#pragma unroll
+        for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (T)(o[j][i][r] * il);
+      }
     }
   }
 }
@@ -545,10 +583,22 @@ template <typename T, int HD>
 void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int* kvl, int B, int S, int H, float scale,
                 uint64_t seed, uint32_t thr, float inv_keep, hipStream_t st) {
   using G = Geo<HD>;
-  const int nqt = (S + BQ - 1) / BQ;
+  // query groups per wave (MIFT_ATTN_QG=1|2).  QG = 2 halves LDS bytes per MFMA but needs
+  // 193 VGPRs (2 waves/SIMD vs 3) and measured slower on MI355X (tools/bench_attn.py: OPT-2.7B
+  // fwd 75.2 vs 69.9 us, distilgpt2 41.0 vs 32.1 us, OPT-6.7B 243 vs 152 us): default 1
+  static const int qg = [] { const char* e = getenv("MIFT_ATTN_QG"); return e ? atoi(e) : 1; }();
   const int smem = G::ROW_BYTES + G::TR_BYTES;
-  hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
-                     (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+  if (qg == 2) {
+    const int nqt = (S + 2 * BQ - 1) / (2 * BQ);
+    hipLaunchKernelGGL((attn_fwd_kernel<T, HD, 2>), dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
+                       (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr,
+                       inv_keep);
+  } else {
+    const int nqt = (S + BQ - 1) / BQ;
+    hipLaunchKernelGGL((attn_fwd_kernel<T, HD, 1>), dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
+                       (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr,
+                       inv_keep);
+  }
 }
 
 template <typename T, int HD>
