@@ -96,10 +96,13 @@ struct TileRegs {
   template <typename T>
   MIFT_HD void load(const T* src, int64_t ld, int row0, int nrows, int tid) {
     using G = Geo<HD>;
+    // 64·CH is a multiple of 64 for every head dim, so the chunk guard is wave-uniform:
+    // test it on the scalar wave index (no per-lane exec-mask branches)
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
     for (int k = 0; k < G::NCH; ++k) {
       const int i = tid + k * 256;
-      if (i < 64 * G::CH) {
+      if ((64 * G::CH) % 256 == 0 || k + 1 < G::NCH || wv * 64 + k * 256 < 64 * G::CH) {
         const int r = i / G::CH, c = i % G::CH;
         const int gr = min(row0 + r, nrows - 1);
         v[k] = *reinterpret_cast<const short8*>(src + (int64_t)gr * ld + c * 8);
@@ -108,10 +111,11 @@ struct TileRegs {
   }
   MIFT_HD void store(char* img, int stride, int tid) const {
     using G = Geo<HD>;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
     for (int k = 0; k < G::NCH; ++k) {
       const int i = tid + k * 256;
-      if (i < 64 * G::CH) {
+      if ((64 * G::CH) % 256 == 0 || k + 1 < G::NCH || wv * 64 + k * 256 < 64 * G::CH) {
         const int r = i / G::CH, c = i % G::CH;
         *reinterpret_cast<short8*>(img + r * stride + c * 16) = v[k];
       }
@@ -166,7 +170,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;                    // [64][HDP] b128 image
   char* Vs = smem + G::ROW_BYTES;     // [64][HD] tr image
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, qc = lane & 15;
   const int nqt = (S + BQB - 1) / BQB;
   const int qt = nqt - 1 - (blockIdx.x % nqt);  // heavy (late) query tiles first
@@ -335,7 +340,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
   char* Ks = smem;                                 // K rows, b128 image (A of S^T)
   char* Vs = smem + G::ROW_BYTES;                  // V rows, b128 image (A of dP^T)
   char* Kt = smem + 2 * G::ROW_BYTES;              // K rows, tr image (B of dQ)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, qc = lane & 15;
   const int nqt = (S + BQ - 1) / BQ;
   const int qt = nqt - 1 - (blockIdx.x % nqt);
@@ -451,7 +457,8 @@ __global__ __launch_bounds__(256, HD <= 64 ? 3 : 1) void attn_bwd_dkdv_kernel(co
   char* dOt = Qt + G::TR_BYTES;                      // dO rows tr image (B of dV)
   float* lse_s = reinterpret_cast<float*>(dOt + G::TR_BYTES);
   float* D_s = lse_s + 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, kc = lane & 15;
   const int nkt = (S + BKV - 1) / BKV;
   const int kt = blockIdx.x % nkt;

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict_
                                                         float* __restrict__ ws) {
   seed = mift_seed(seed, sstep);
   __shared__ float red[NW][32][33];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, fr = lane & 15;
   const int mb = blockIdx.x / KS, kss = blockIdx.x % KS;
   const int m0 = mb * 32;
@@ -200,7 +201,8 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X
   constexpr int NB = 4;
   __shared__ __attribute__((aligned(16))) char Xs[NB][32 * XS];
   __shared__ __attribute__((aligned(16))) char Ys[NB][32 * YS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, li = lane & 15;
   const int ntp = P / 64;
   const int pt = blockIdx.x % ntp, ms = blockIdx.x / ntp;
