@@ -402,6 +402,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
       vr.load(Vg, ld, k0 + BKV, S, tid);
     }
     vec8<T> dsf[2];
+    const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       float4_ sa = float4_{0.f, 0.f, 0.f, 0.f}, pa = float4_{0.f, 0.f, 0.f, 0.f};
@@ -418,8 +419,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = k0 + t * 16 + g * 4 + r;
-        const float p = (key > myq || key >= klen) ? 0.f : fast_exp2(sa[r] * c2 - lse2);
+        float p = fast_exp2(sa[r] * c2 - lse2);
+        if (diag) {  // wave-uniform: interior tiles skip the per-element causal / padding mask
+          const int key = k0 + t * 16 + g * 4 + r;
+          if (key > myq || key >= klen) p = 0.f;
+        }
         float dp = pa[r];
         if (thr != 0) dp = kp[r] ? dp * inv_keep : 0.f;
         dsf[t >> 1][(t & 1) * 4 + r] = (T)(p * (dp - Dq));
@@ -513,6 +517,8 @@ __global__ __launch_bounds__(256, HD <= 64 ? 3 : 1) void attn_bwd_dkdv_kernel(co
       dr.load(dOg, D, qb + BQ, S, tid);
     }
     vec8<T> pf[2], dsf[2];
+    // wave-uniform: every query of the tile sees every key of this wave (no causal / length mask)
+    const bool interior = qb >= k0 + 15 && qb + BQ <= S && k0 + 16 <= klen;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       float4_ sa = float4_{0.f, 0.f, 0.f, 0.f}, pa = float4_{0.f, 0.f, 0.f, 0.f};
@@ -549,8 +555,12 @@ __global__ __launch_bounds__(256, HD <= 64 ? 3 : 1) void attn_bwd_dkdv_kernel(co
       for (int r = 0; r < 4; ++r) {
         const int ql = t * 16 + g * 4 + r;
         const int q = qb + ql;
-        const bool valid = q < S && mykey <= q && mykey < klen;
-        const float p = valid ? fast_exp2(sa[r] * c2 - lse_s[ql]) : 0.f;
+        bool valid = true;
+        float p = fast_exp2(sa[r] * c2 - lse_s[ql]);
+        if (!interior) {
+          valid = q < S && mykey <= q && mykey < klen;
+          if (!valid) p = 0.f;
+        }
         float pd = p, dp = pa[r];
         if (thr != 0) {
           const uint32_t bits = (S & 1) ? mift_bits16(seed, ((uint64_t)bh * S + q) * S + mykey)
