@@ -97,6 +97,7 @@ def test_xent_fwd_bwd(V, ldV):
     logits = (torch.randn(M, ldV, device="cuda") * 3).to(torch.bfloat16)
     labels = torch.randint(0, V, (M,), device="cuda")
     labels[::7] = -100
+    labels[1], labels[2] = V - 1, 0  # first / last column (tail chunk)
     x = logits[:, :V].float().requires_grad_(True)
     ref_loss = torch.nn.functional.cross_entropy(x, labels, ignore_index=-100, reduction="none")
     ref_loss.sum().backward()

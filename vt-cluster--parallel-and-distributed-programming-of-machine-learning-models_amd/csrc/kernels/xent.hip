@@ -111,6 +111,9 @@ __global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, c
   T* x = logits + (int64_t)row * ldV;
   short8 v[NV];
   float m = -INFINITY;
+  // Only the chunk holding column V-1 needs the per-element `< V` test; every
+  // other chunk takes the branch-free path (VALU, not HBM, bounds this kernel:
+  // ~2 exp + ~12 ALU ops per logit).
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = (k * 512 + tid) * 8;
@@ -118,9 +121,14 @@ __global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, c
       v[k] = *reinterpret_cast<const short8*>(x + c);
       float f[8];
       load8<T>(reinterpret_cast<const T*>(&v[k]), f);
+      if (c + 8 <= V) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (c + e < V) m = fmaxf(m, f[e]);
+        for (int e = 0; e < 8; ++e) m = fmaxf(m, f[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (c + e < V) m = fmaxf(m, f[e]);
+      }
     }
   }
   const int64_t lab = labels[row];
@@ -133,6 +141,12 @@ __global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, c
 #pragma unroll
   for (int i = 1; i < 8; ++i) M = fmaxf(M, red[i]);
   __syncthreads();
+  // exp(f - M) = exp2(f*log2e - M*log2e): one FMA feeding v_exp_f32
+  constexpr float L2E = 1.4426950408889634f;
+  const float Ml = M * L2E;
+  // Pass 2 overwrites each register vector with e = exp(f - M) rounded to T
+  // (zero past V), so pass 3 is one multiply by 1/S per logit instead of a
+  // second FMA + v_exp (softmax rel. error <= 2^-8, below the bf16 output's).
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -140,9 +154,23 @@ __global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, c
     if (c < ldV) {
       float f[8];
       load8<T>(reinterpret_cast<const T*>(&v[k]), f);
+      if (c + 8 <= V) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (c + e < V) s += __expf(f[e] - M);
+        for (int e = 0; e < 8; ++e) f[e] = __builtin_amdgcn_exp2f(fmaf(f[e], L2E, -Ml));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = (c + e < V) ? __builtin_amdgcn_exp2f(fmaf(f[e], L2E, -Ml)) : 0.f;
+      }
+      short8 pk;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s += f[e];
+        T t = (T)f[e];
+        short sh;
+        __builtin_memcpy(&sh, &t, 2);
+        pk[e] = sh;
+      }
+      v[k] = pk;
     }
   }
   s = wave_sum(s);
@@ -157,6 +185,7 @@ __global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, c
     if (lse_out) lse_out[row] = lse;
   }
   if (!write_grad) return;
+  const float inv_s = valid ? 1.f / S : 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = (k * 512 + tid) * 8;
@@ -164,11 +193,12 @@ __global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, c
       float f[8];
       load8<T>(reinterpret_cast<const T*>(&v[k]), f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int cc = c + e;
-        float p = (valid && cc < V) ? __expf(f[e] - lse) : 0.f;
-        if (valid && cc == lab) p -= 1.f;
-        f[e] = p;
+      for (int e = 0; e < 8; ++e) f[e] *= inv_s;
+      const unsigned d = (unsigned)(lab - c);
+      if (valid && d < 8u) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((unsigned)e == d) f[e] -= 1.f;
       }
       store8<T>(x + c, f);
     }
