@@ -27,8 +27,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="distilgpt2")
     ap.add_argument("--seq_len", type=int, default=None, help="default 256 (GPT-2) / 512 (OPT, P2 sbatch)")
     ap.add_argument("--batch", type=int, default=1)
@@ -43,6 +43,11 @@ def main():
                     help="fused = mift HIP kernels; torch = eager PyTorch ops on the same model (comparison)")
     ap.add_argument("--profile_dir", default=None, help="torch.profiler chrome trace of 3 steps")
     a = ap.parse_args()
+    # RCCL / Gloo print their init banners on fd 1 from native code; route
+    # everything but the result line to stderr so stdout is exactly ONE JSON line.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     if a.impl == "torch":
         os.environ["MIFT_KERNELS"] = "0"
@@ -159,7 +164,8 @@ def main():
                        "tokens_per_gpu_per_s": round(value / n, 1),
                        "final_grad_norm": round(stats["grad_norm"], 4)},
         }
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     D.destroy()
 
 
