@@ -89,12 +89,13 @@ def test_gemm_nt_act_backward(act):
     torch.testing.assert_close(out.float(), exp.float(), atol=5e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("V,ldV", [(1000, 1024), (50257, 50304)])
-def test_xent_fwd_bwd(V, ldV):
+@pytest.mark.parametrize("V,ldV,dtype", [(1000, 1024, torch.bfloat16), (50257, 50304, torch.bfloat16),
+                                         (50272, 50272, torch.float16), (3000, 3008, torch.float16)])
+def test_xent_fwd_bwd(V, ldV, dtype):
     C = _C()
     torch.manual_seed(4)
     M = 64
-    logits = (torch.randn(M, ldV, device="cuda") * 3).to(torch.bfloat16)
+    logits = (torch.randn(M, ldV, device="cuda") * 3).to(dtype)
     labels = torch.randint(0, V, (M,), device="cuda")
     labels[::7] = -100
     labels[1], labels[2] = V - 1, 0  # first / last column (tail chunk)

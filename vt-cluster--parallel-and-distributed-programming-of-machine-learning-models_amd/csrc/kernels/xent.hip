@@ -205,6 +205,27 @@ __global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, c
   }
 }
 
+// NV = register vectors per thread (row width <= NV*4096); the exact-fit
+// instantiations cover GPT-2 (50304 padded -> 13) and OPT (50272 -> 13).
+template <typename T>
+void xent_reg_launch(at::Tensor& logits, const at::Tensor& lab, at::Tensor& loss, at::Tensor& lse, int V, int ldV,
+                     int nv, int64_t ignore_index, bool write_grad, int M, hipStream_t st) {
+  T* x = reinterpret_cast<T*>(logits.data_ptr());
+  const int64_t* l = lab.data_ptr<int64_t>();
+  float* lo = loss.data_ptr<float>();
+  float* ls = lse.data_ptr<float>();
+  const int wg = write_grad ? 1 : 0;
+#define XR(N) xent_reg_kernel<T, N><<<M, 512, 0, st>>>(x, l, lo, ls, V, ldV, ignore_index, wg)
+  if (nv <= 1) XR(1);
+  else if (nv <= 2) XR(2);
+  else if (nv <= 4) XR(4);
+  else if (nv <= 8) XR(8);
+  else if (nv <= 12) XR(12);
+  else if (nv == 13) XR(13);
+  else XR(16);
+#undef XR
+}
+
 }  // namespace
 
 // logits [M, ldV] (modified in place into dlogits when write_grad) -> (loss[M], lse[M])
@@ -220,17 +241,10 @@ std::vector<at::Tensor> mift_xent_fwd_bwd(at::Tensor& logits, const at::Tensor& 
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   auto lab = labels.contiguous();
   const int nv = (ldV + 4095) / 4096;
-  if (logits.scalar_type() == at::kBFloat16 && nv <= 16) {
-#define XR(N) case N: xent_reg_kernel<bf16, N><<<M, 512, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), \
-                                                   loss.data_ptr<float>(), lse.data_ptr<float>(), (int)V, ldV, \
-                                                   ignore_index, write_grad ? 1 : 0); break;
-    switch (nv) { XR(1) XR(2) XR(4) XR(8) XR(12) XR(13) XR(16)
-      default:
-        if (nv <= 4) { xent_reg_kernel<bf16, 4><<<M, 512, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0); }
-        else if (nv <= 8) { xent_reg_kernel<bf16, 8><<<M, 512, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0); }
-        else { xent_reg_kernel<bf16, 16><<<M, 512, 0, st>>>((bf16*)logits.data_ptr(), lab.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), (int)V, ldV, ignore_index, write_grad ? 1 : 0); }
-    }
-#undef XR
+  const bool is_bf = logits.scalar_type() == at::kBFloat16, is_h = logits.scalar_type() == at::kHalf;
+  if ((is_bf || is_h) && nv <= 16) {
+    if (is_bf) xent_reg_launch<bf16>(logits, lab, loss, lse, (int)V, ldV, nv, ignore_index, write_grad, M, st);
+    else xent_reg_launch<fp16>(logits, lab, loss, lse, (int)V, ldV, nv, ignore_index, write_grad, M, st);
     return {loss, lse};
   }
   if (logits.scalar_type() == at::kBFloat16)
