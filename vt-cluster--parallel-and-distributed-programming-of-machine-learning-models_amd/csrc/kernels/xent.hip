@@ -112,8 +112,8 @@ __global__ __launch_bounds__(512) void xent_reg_kernel(T* __restrict__ logits, c
   short8 v[NV];
   float m = -INFINITY;
   // Only the chunk holding column V-1 needs the per-element `< V` test; every
-  // other chunk takes the branch-free path (VALU, not HBM, bounds this kernel:
-  // ~2 exp + ~12 ALU ops per logit).
+  // other chunk takes the branch-free path (keeps the ALU work per logit near
+  // its floor of ~2 exp + ~10 ops).
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = (k * 512 + tid) * 8;
