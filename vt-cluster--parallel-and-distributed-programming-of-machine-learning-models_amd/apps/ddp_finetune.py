@@ -128,7 +128,9 @@ def main(argv=None, defaults=None):
     mb, acc = (args.batch * args.accum, 1) if fold else (args.batch, args.accum)
     stamp = datetime.datetime.now().strftime("%Y%m%d-%H%M%S")
     base = args.model.split("/")[-1]
-    run_name = args.run_name or f"{base}_lora_{args.dataset}_N{world}_{stamp}"
+    # rank 0's clock names the run for everyone: per-rank stamps can straddle a second (or differ
+    # across nodes) and then checkpoints / resume='auto' would use different directories per rank
+    run_name = D.broadcast_obj(args.run_name or f"{base}_lora_{args.dataset}_N{world}_{stamp}")
     save_dir = os.path.join(args.out_root, run_name)
     batcher = MicroBatcher(ds, mb, acc, rank=ctx.dp_rank, world=ctx.dp, mode="strided")
     tcfg = TrainConfig(epochs=args.epochs, batch=mb, accum=acc, lr=args.lr, precision=precision,

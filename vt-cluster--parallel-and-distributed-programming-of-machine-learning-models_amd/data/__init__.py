@@ -63,6 +63,27 @@ class TokenDataset:
         return TokenDataset(ids, lens, pad, vocab)
 
 
+def row_label_tokens(ds: "TokenDataset") -> np.ndarray:
+    """[N] int64: per-row count of shifted causal-LM targets (labels[1:] != -100, see lm_labels)."""
+    cached = getattr(ds, "_row_label_tokens", None)
+    if cached is not None:
+        return cached
+    S = ds.ids.shape[1]
+    out = np.empty(len(ds), dtype=np.int64)
+    cols = np.arange(1, S)[None, :]
+    for r0 in range(0, len(ds), 16384):  # bounded temporaries on large corpora
+        ids = ds.ids[r0:r0 + 16384, 1:]
+        lens = ds.lengths[r0:r0 + 16384, None]
+        out[r0:r0 + len(ids)] = ((cols < lens) & (ids != ds.pad_id)).sum(axis=1)
+    ds._row_label_tokens = out
+    return out
+
+
+class StepBatch(list):
+    """The micro-batches of one optimizer step; ``global_tokens`` = label tokens over all DP ranks."""
+    global_tokens = None
+
+
 def lm_labels(ids: torch.Tensor, mask: torch.Tensor, pad_id: int) -> torch.Tensor:
     """Causal-LM labels: input_ids with padding (and pad-id tokens) -> -100."""
     lab = ids.clone()
@@ -177,8 +198,34 @@ class MicroBatcher:
         self.prefetch = prefetch
         self._loader = None
 
-    def indices(self, epoch=0):
-        return shard_indices(len(self.ds), self.rank, self.world, self.mode, self.shuffle, self.seed, epoch)
+    def indices(self, epoch=0, rank=None):
+        r = self.rank if rank is None else rank
+        return shard_indices(len(self.ds), r, self.world, self.mode, self.shuffle, self.seed, epoch)
+
+    def global_step_tokens(self, epoch=0):
+        """[steps] int64: shifted causal-LM label tokens of each optimizer step summed over ALL DP ranks.
+
+        The shard plan is deterministic, so every rank computes the same counts locally: the
+        token-normalised loss needs no per-step collective (the reference Trainer all-gathers
+        ``num_items_in_batch`` every step)."""
+        key = (epoch,)
+        if getattr(self, "_gst", (None,))[0] == key:
+            return self._gst[1]
+        rows = row_label_tokens(self.ds)
+        per = self.mb * self.accum
+        tot = None
+        for r in range(self.world):
+            idx = self.indices(epoch, rank=r)
+            c = rows[idx]
+            starts = np.arange(0, len(c), per)
+            s = np.add.reduceat(c, starts) if len(c) else np.zeros(0, np.int64)
+            if tot is None:
+                tot = s
+            else:  # contiguous shards may differ by a step between ranks: zero-pad the shorter
+                n = max(len(tot), len(s))
+                tot = np.pad(tot, (0, n - len(tot))) + np.pad(s, (0, n - len(s)))
+        self._gst = (key, tot.astype(np.int64))
+        return self._gst[1]
 
     def steps_per_epoch(self):
         n = len(self.indices(0))
@@ -197,7 +244,7 @@ class MicroBatcher:
         n_mb = (len(idx) + self.mb - 1) // self.mb
         first = start_step * self.accum
         self._loader.start(torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)), first)
-        step_mbs, j = [], first
+        step_mbs, j = StepBatch(), first
         while True:
             item = self._loader.next()
             if not item:
@@ -206,15 +253,19 @@ class MicroBatcher:
             j += 1
             if len(step_mbs) == self.accum or j == n_mb:
                 yield step_mbs
-                step_mbs = []
+                step_mbs = StepBatch()
 
     def epoch(self, epoch=0, start_step=0):
         idx = self.indices(epoch)
-        if self.native:
-            yield from self._native_epoch(idx, start_step)
-            return
+        gtok = self.global_step_tokens(epoch)
+        it = self._native_epoch(idx, start_step) if self.native else self._py_epoch(idx, start_step)
+        for s, step_mbs in enumerate(it, start=start_step):
+            step_mbs.global_tokens = int(gtok[s]) if s < len(gtok) else None
+            yield step_mbs
+
+    def _py_epoch(self, idx, start_step):
         n_mb = (len(idx) + self.mb - 1) // self.mb
-        step_mbs = []
+        step_mbs = StepBatch()
         for j in range(n_mb):
             b = self.ds.batch(idx[j * self.mb:(j + 1) * self.mb])
             if self.pin:
@@ -224,7 +275,7 @@ class MicroBatcher:
                 step_no = j // self.accum
                 if step_no >= start_step:
                     yield step_mbs
-                step_mbs = []
+                step_mbs = StepBatch()
 
 
 def _native_loader_available():

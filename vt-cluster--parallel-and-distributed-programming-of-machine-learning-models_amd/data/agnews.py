@@ -7,8 +7,10 @@ Reference (`labs/tiny/train_tiny.py:132-141`, `infer_ddp.py:43-49`,
 
   * the splits are read straight from an HF datasets cache (``ag_news-*.arrow``
     Arrow IPC stream files, via pyarrow — nothing is unpickled) found under
-    ``$HF_HOME``, ``./.hf_cache``, ``~/.cache/huggingface`` or
-    ``$MIFT_HF_CACHE``;
+    ``$MIFT_HF_CACHE``, ``$HF_HOME``, ``./.hf_cache`` or
+    ``~/.cache/huggingface`` (the product never reads the reference tree; to
+    reproduce the reference's own AG-News slice point ``MIFT_HF_CACHE`` at a
+    copy of its ``.hf_cache``);
   * when only the test split is cached (as in the reference's own
     ``.hf_cache``, whose train shard is a missing large blob), "train" is
     served from test rows [2048:] — disjoint from every eval slice the labs
@@ -34,7 +36,7 @@ def cache_roots():
     if os.environ.get("MIFT_AGNEWS") == "synthetic":
         return []
     roots = [os.environ.get("MIFT_HF_CACHE"), os.environ.get("HF_HOME"), os.path.join(os.getcwd(), ".hf_cache"),
-             os.path.expanduser("~/.cache/huggingface"), "/root/reference/.hf_cache"]
+             os.path.expanduser("~/.cache/huggingface")]
     return [r for r in roots if r and os.path.isdir(r)]
 
 

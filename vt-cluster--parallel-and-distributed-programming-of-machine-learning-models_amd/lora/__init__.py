@@ -121,6 +121,7 @@ class LoraArena:
             p.grad = self.grad[o:o + p.numel()].view_as(p)
         self.model = model
         self.version = 0  # bumped whenever the parameters change (optimizer step, load)
+        self.grad_ready = None  # fused-backward readiness callback (offsets) set by the DP reducer
         # bind every adapted Linear to its arena slices (fused path writes grads in place)
         off_of = {id(p): o for (_, p), o in zip(self.named, self.offsets)}
         self.modules = []

@@ -59,6 +59,15 @@ def _mask_proj(g2, p, seed, lo):
 _BWD = {0: 0, 1: 4, 2: 5, 3: 6}
 
 
+def _notify(arena, offsets):
+    """Tell the DP reducer (mift.parallel.ddp) that these arena grads are final for this
+    micro-step: the wgrad kernels are queued, so its bucket all-reduce can launch now and
+    overlap the rest of backward (the fused path never runs AccumulateGrad hooks)."""
+    cb = getattr(arena, "grad_ready", None)
+    if cb is not None:
+        cb(offsets)
+
+
 class AdapterOps:
     """Packed 16-bit operands of ONE adapter (rank padded to 32).
 
@@ -104,6 +113,7 @@ class AdapterOps:
                 K.lora_wgrad_into(gz, T32, g, 1, r, offB)              # dB [N,r]
                 K.lora_wgrad_into(x, dT32, g, 2, r, offA, p, seed)     # dA [r,K]
             run_side(gz.device, wgrad, gz, T32, x, dT32)
+            _notify(self.arena, (offA, offB))
             return [None, None], dT32
         dBf = K.lora_wgrad(gz, T32)
         dAf = K.lora_wgrad(x, dT32, p=p, seed=seed)
@@ -175,6 +185,7 @@ class MultiAdapterOps:
                     K.lora_wgrad_into(gz[:, n0:n1], T32, g, 1, l.lora_r, l._offB, qoff=q)
                     K.lora_wgrad_into(x, dT32, g, 2, l.lora_r, l._offA, p, seed, qoff=q)
             run_side(gz.device, wgrad, gz, T32, x, dT32)
+            _notify(self.arena, [o for l, _, _, _ in slots for o in (l._offA, l._offB)])
             return [None, None] * len(slots), dT32
         dAf = K.lora_wgrad(x, dT32, p=p, seed=seed)
         for l, n0, n1, q in self.slots:

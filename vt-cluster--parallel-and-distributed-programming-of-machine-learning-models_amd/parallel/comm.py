@@ -1,10 +1,14 @@
-"""Collective / point-to-point helpers that pick the right primitive per backend.
+"""Collective / point-to-point helpers: ONE call path for RCCL and Gloo.
 
-RCCL (backend "nccl" on ROCm) moves device tensors directly over xGMI and
-orders work on the current HIP stream (``Work.wait()`` makes the stream wait;
-the host does not block).  Gloo — the CPU plumbing backend, also used to
-rehearse multi-rank pipelines on a single GPU box — only moves host tensors,
-so device tensors are staged through pinned host memory there.
+Every backend goes through the same torch.distributed calls —
+``batch_isend_irecv`` for pipeline p2p, ``reduce_scatter_tensor`` /
+``all_gather_into_tensor`` for ZeRO-1 — so the multi-process Gloo tests on
+the CPU exercise exactly the op grouping, ordering and shapes that RCCL runs
+over xGMI.  The only backend difference is host staging: Gloo moves host
+tensors, so device tensors are copied through host memory around the call
+(the GPU-box rehearsal of multi-rank schedules on one device); RCCL moves
+device tensors directly and orders its work against the current HIP stream
+(``Work.wait()`` makes the stream wait; the host does not block).
 
 Reference parity: DeepSpeed's pipeline p2p (``deepspeed.runtime.pipe.p2p``,
 [lib]) and ZeRO-1 reduce-scatter / all-gather (X13).
@@ -17,67 +21,81 @@ def backend_of(group=None):
     return dist.get_backend(group) if dist.is_initialized() else "none"
 
 
-def _host_staged(group):
-    return backend_of(group) == "gloo"
+def _host_staged(group, *tensors):
+    return backend_of(group) == "gloo" and any(t.is_cuda for t in tensors)
+
+
+class Pending:
+    """Outstanding p2p exchange: ``wait()`` completes it and returns the received tensors."""
+
+    def __init__(self, works, recvs, copies, keep):
+        self._works, self._recvs, self._copies, self._keep = works, recvs, copies, keep
+        self.done = False
+
+    def wait(self):
+        if not self.done:
+            for w in self._works:
+                w.wait()
+            for dst, src in self._copies:  # host-staged receives land in their device tensors
+                dst.copy_(src, non_blocking=False)
+            self._works, self._keep, self.done = [], None, True
+        return self._recvs
 
 
 class P2P:
-    """Paired send/recv between adjacent pipeline stages (global ranks)."""
+    """Grouped send/recv between pipeline stages (global ranks).
+
+    ``group`` selects the communicator; the pipeline engine uses one group per
+    DIRECTION (activations s→s+1, gradients s+1→s) so that a receive posted
+    early on one direction never queues behind a send on the other (RCCL runs
+    the p2p of one communicator and peer pair in issue order on one stream)."""
 
     def __init__(self, group=None):
         self.group = group
-        self.gloo = _host_staged(group)
+
+    def post(self, sends=(), recvs=()):
+        """Issue ``sends`` [(tensor, dst)] and ``recvs`` [(tensor, src)] as ONE batch_isend_irecv."""
+        sends, recvs = list(sends), list(recvs)
+        if not sends and not recvs:
+            return Pending([], [], [], None)
+        staged = _host_staged(self.group, *[t for t, _ in sends + recvs])
+        ops, copies, keep = [], [], []
+        for t, peer in sends:
+            src = t.detach()
+            if staged and src.is_cuda:
+                src = src.to("cpu")
+            keep.append(src)
+            ops.append(dist.P2POp(dist.isend, src.contiguous(), peer, group=self.group))
+        for t, peer in recvs:
+            dst = t
+            if staged and t.is_cuda:
+                dst = torch.empty(t.shape, dtype=t.dtype)
+                copies.append((t, dst))
+            keep.append(dst)
+            ops.append(dist.P2POp(dist.irecv, dst, peer, group=self.group))
+        works = dist.batch_isend_irecv(ops)
+        return Pending(works, [t for t, _ in recvs], copies, keep)
 
     def exchange(self, sends=(), recvs=()):
-        """sends: [(tensor, dst)], recvs: [(tensor, src)] -> completes all, returns recv tensors.
-
-        NCCL/RCCL: one ``batch_isend_irecv`` (grouped, deadlock-free for the
-        1F1B send-fwd/recv-bwd pairs); gloo: host copies + isend/irecv."""
-        if not sends and not recvs:
-            return []
-        if not self.gloo:
-            ops = [dist.P2POp(dist.isend, t, peer, group=self.group) for t, peer in sends]
-            ops += [dist.P2POp(dist.irecv, t, peer, group=self.group) for t, peer in recvs]
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-            return [t for t, _ in recvs]
-        works, stage = [], []
-        for t, peer in sends:
-            h = t.detach().to("cpu") if t.is_cuda else t.detach().contiguous()
-            stage.append(h)
-            works.append(dist.isend(h, peer, group=self.group))
-        outs = []
-        for t, peer in recvs:
-            h = torch.empty(t.shape, dtype=t.dtype) if t.is_cuda else t
-            outs.append((t, h))
-            works.append(dist.irecv(h, peer, group=self.group))
-        for w in works:
-            w.wait()
-        for t, h in outs:
-            if h is not t:
-                t.copy_(h)
-        return [t for t, _ in recvs]
+        """Blocking form of :meth:`post` (returns the received tensors)."""
+        return self.post(sends, recvs).wait()
 
 
 def reduce_scatter_flat(out, inp, group):
     """out[i] = sum over ranks of inp[rank_idx*n + i]   (n = out.numel())."""
-    if backend_of(group) == "gloo":
-        buf = inp.clone()
-        dist.all_reduce(buf, group=group)
-        r = dist.get_rank(group)
-        out.copy_(buf[r * out.numel():(r + 1) * out.numel()])
+    if _host_staged(group, out, inp):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.reduce_scatter_tensor(h, inp.detach().cpu(), group=group)
+        out.copy_(h)
     else:
         dist.reduce_scatter_tensor(out, inp, group=group)
 
 
 def all_gather_flat(out, shard, group):
     """out = concat over ranks of shard."""
-    if backend_of(group) == "gloo":
-        n = shard.numel()
-        views = [out[i * n:(i + 1) * n] for i in range(dist.get_world_size(group))]
-        tmp = [torch.empty_like(shard) for _ in views]
-        dist.all_gather(tmp, shard.contiguous(), group=group)
-        for v, t in zip(views, tmp):
-            v.copy_(t)
+    if _host_staged(group, out, shard):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, shard.detach().cpu().contiguous(), group=group)
+        out.copy_(h)
     else:
         dist.all_gather_into_tensor(out, shard.contiguous(), group=group)

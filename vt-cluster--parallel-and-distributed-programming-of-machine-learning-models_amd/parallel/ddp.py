@@ -5,11 +5,14 @@ for LoRA on MI355X:
   * no parameter broadcast at construction: every rank builds identical
     weights from the same seed / file, and ``verify_replicas`` checks a
     checksum (all-reduce of MAX-MIN) instead of broadcasting 329 MB (X6);
-  * the gradient arena is split into buckets in *reverse* module order; a
-    post-accumulate-grad hook counts readiness and launches each bucket's
-    async all-reduce (SUM — the loss is already normalised by the global
-    token count) as soon as its last tensor is done, overlapping the rest
-    of backward; ``finish()`` waits for all handles;
+  * the gradient arena is split into buckets in *reverse* module order;
+    readiness is counted per tensor and each bucket's async all-reduce (SUM —
+    the loss is already normalised by the global token count) launches as
+    soon as its last tensor is done, overlapping the rest of backward;
+    ``finish()`` waits for all handles.  Readiness comes from two sources:
+    the fused GPU blocks write LoRA grads straight into the arena and call
+    ``arena.grad_ready(offsets)`` after queueing an adapter's wgrad kernels
+    (mift.ops.fused), the eager path from post-accumulate-grad hooks;
   * ``no_sync()`` for accumulation micro-steps (reference ``no_sync`` on
     steps 1..accum-1, verified in SURVEY C16);
   * default bucket 25 MB: distilgpt2 LoRA (1.6 MB fp32) and OPT-2.7B
@@ -47,15 +50,19 @@ class GradReducer:
         for b in buckets:
             lo = min(off for _, off in b)
             hi = max(off + p.numel() for p, off in b)
-            self.buckets.append({"params": [p for p, _ in b], "lo": lo, "hi": hi, "pending": len(b)})
+            self.buckets.append({"params": [p for p, _ in b], "lo": lo, "hi": hi, "pending": len(b),
+                                 "idx": len(self.buckets)})
         self._p2b = {}
         for i, b in enumerate(self.buckets):
             for p in b["params"]:
                 self._p2b[id(p)] = i
+        self._off2p = {off: p for (_, p), off in named}
         self._hooks = []
+        self.launch_log = []  # (bucket index, "backward" | "finish") per launch of the last step
         if self.overlap:
             for _, p in arena.named:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+            arena.grad_ready = self._on_ready_offsets
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -66,55 +73,92 @@ class GradReducer:
         finally:
             self._sync = old
 
-    def _launch(self, b):
+    def _launch(self, b, where="finish"):
+        if where == "backward" and self.arena.grad.is_cuda:
+            from ..ops.streams import join
+            join()  # wgrad kernels queued on the side stream are ordered before the collective
         sl = self.arena.grad[b["lo"]:b["hi"]]
         self.handles.append(dist.all_reduce(sl, group=self.group, async_op=True))
+        b["launched"] = True
+        self.launch_log.append((b["idx"], where))
 
-    def _on_grad(self, p):
+    def _ready(self, p):
         if not self._sync or not self.overlap:
             return
         b = self.buckets[self._p2b[id(p)]]
         b["pending"] -= 1
-        if b["pending"] == 0:
-            self._launch(b)
+        if b["pending"] == 0 and not b.get("launched"):
+            self._launch(b, "backward")
+
+    def _on_grad(self, p):
+        self._ready(p)
+
+    def _on_ready_offsets(self, offsets):
+        """Fused-backward notification: the arena slices at ``offsets`` hold this micro-step's grads."""
+        for off in offsets:
+            p = self._off2p.get(off)
+            if p is not None:
+                self._ready(p)
 
     def finish(self):
         """Call after the last micro-batch's backward of an optimizer step."""
         if not self.enabled:
             return
-        if self.overlap:
-            for b in self.buckets:
-                if b["pending"] > 0:  # params that got no grad this step (unused) -> launch anyway
-                    self._launch(b)
-        else:
-            for b in self.buckets:
+        for b in self.buckets:
+            if not b.get("launched"):  # no overlap, or params that got no grad this step
                 self._launch(b)
         for h in self.handles:
             h.wait()
         self.handles = []
         for b in self.buckets:
             b["pending"] = len(b["params"])
+            b["launched"] = False
+
+    def begin_step(self):
+        self.launch_log = []
 
     def remove(self):
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if getattr(self.arena, "grad_ready", None) == self._on_ready_offsets:
+            self.arena.grad_ready = None
 
 
 @torch.no_grad()
-def verify_replicas(tensors, group=None, atol=0.0):
-    """Checksum every tensor across the group; raise if replicas diverge.
+def replica_checksum(tensors):
+    """[n, 2] int64: per tensor, the wrapping sums of its raw bit patterns and of the bit patterns
+    weighted by position — exact (no float rounding), sensitive to sign-symmetric drift and to a
+    small tensor differing next to large ones."""
+    rows = []
+    chunk = 1 << 24  # bounded int64 temporaries (OPT-6.7B frozen weights are 6.7 G elements)
+    for t in tensors:
+        t = t.detach().contiguous().reshape(-1)
+        ib = {1: torch.int8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[t.element_size()]
+        flat = t.view(ib)
+        acc = torch.zeros(2, dtype=torch.int64, device=t.device)
+        for c0 in range(0, flat.numel(), chunk):
+            bits = flat[c0:c0 + chunk].to(torch.int64)
+            w = (torch.arange(c0, c0 + bits.numel(), device=bits.device, dtype=torch.int64) % 65521) + 1
+            acc += torch.stack([bits.sum(), (bits * w).sum()])
+        rows.append(acc)
+    return torch.stack(rows) if rows else torch.zeros(0, 2, dtype=torch.int64)
 
-    Replaces DDP's construction-time broadcast: identical init by seed,
-    verified with one all-reduce of [max, -min] of per-tensor sums."""
+
+@torch.no_grad()
+def verify_replicas(tensors, group=None):
+    """Checksum every tensor across the group; raise unless all replicas are bit-identical.
+
+    Replaces DDP's construction-time broadcast: identical init by seed, verified with one
+    all-reduce of [max, -min] of the exact per-tensor checksums (RCCL all-reduce results are
+    identical on every rank, so trained replicas must stay bit-equal too)."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return True
-    sums = torch.stack([t.detach().float().sum() for t in tensors])
-    mx = sums.clone()
-    mn = -sums.clone()
-    both = torch.stack([mx, mn])
+    cs = replica_checksum(tensors)
+    both = torch.stack([cs, -cs])
     dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
-    spread = (both[0] + both[1]).abs().max().item()
-    if spread > atol + 1e-3 * sums.abs().max().item():
-        raise RuntimeError(f"replica divergence detected: max checksum spread {spread}")
+    spread = both[0] + both[1]
+    if bool((spread != 0).any()):
+        bad = [i for i in range(spread.shape[0]) if bool((spread[i] != 0).any())]
+        raise RuntimeError(f"replica divergence detected: {len(bad)} tensor(s) differ, first index {bad[0]}")
     return True

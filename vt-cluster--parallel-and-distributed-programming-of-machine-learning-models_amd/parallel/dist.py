@@ -73,6 +73,8 @@ class DistContext:
     pp_ranks: List[int] = field(default_factory=list)
     timeout: Optional[object] = None        # collective timeout (watchdog) for every group
     dp_ranks: List[int] = field(default_factory=list)
+    pp_fwd_group: Optional[object] = None   # p2p: activations stage s -> s+1
+    pp_bwd_group: Optional[object] = None   # p2p: activation grads stage s+1 -> s
 
     @property
     def is_main(self):
@@ -169,9 +171,15 @@ def build_grid(ctx: DistContext, pp: int):
     # every rank must create every group in the same order
     for r in range(dp):
         ranks = list(range(r * pp, (r + 1) * pp))
-        g = dist.new_group(ranks, timeout=ctx.timeout) if pp > 1 and world > 1 else None
+        multi = pp > 1 and world > 1
+        g = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
+        # one p2p communicator per direction (activations s->s+1, gradients s+1->s): a receive
+        # posted early on one direction never queues behind the other direction's send
+        gf = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
+        gb = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
         if ctx.rank in ranks:
             ctx.pp_group, ctx.pp_ranks = g, ranks
+            ctx.pp_fwd_group, ctx.pp_bwd_group = gf, gb
     for s in range(pp):
         ranks = list(range(s, world, pp))
         g = dist.new_group(ranks, timeout=ctx.timeout) if dp > 1 and world > 1 else None
@@ -197,6 +205,18 @@ def barrier():
     if dist.is_initialized():
         c = get()
         dist.barrier(group=c.ctrl_group)
+
+
+def broadcast_obj(obj, src: int = 0):
+    """Rank ``src``'s picklable ``obj`` on every rank (gloo control plane; identity when single).
+
+    Used for run-wide choices that must not depend on a per-rank clock or environment
+    (e.g. the run directory name: every rank must checkpoint into the same place)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return obj
+    box = [obj]
+    dist.broadcast_object_list(box, src=src, group=get().ctrl_group)
+    return box[0]
 
 
 def destroy():

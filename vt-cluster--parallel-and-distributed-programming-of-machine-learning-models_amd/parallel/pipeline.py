@@ -19,9 +19,11 @@ design that also fixes its defects:
   * the schedule is non-interleaved 1F1B (DeepSpeed ``TrainSchedule``): warm-up
     ``S - s - 1`` forwards, steady one-forward-one-backward, cool-down; at most
     ``S - s`` micro-batches of activations are alive on stage s;
-  * adjacent-stage transfers are one grouped ``batch_isend_irecv`` per
-    exchange (send-activation + recv-gradient together), which RCCL runs on
-    its own stream over the direct xGMI link between the two GPUs.
+  * adjacent-stage transfers are ``batch_isend_irecv`` posts on one
+    communicator per direction (activations forward, gradients backward), so
+    a receive can be posted ahead of the compute that needs it without ever
+    queueing behind the other direction's send; RCCL runs them on their own
+    streams over the direct xGMI link, into reused ring buffers.
 
 Loss normalisation: the last stage scales each micro-batch's summed token
 loss by ``loss_scale / global_ntokens`` (token-count normalisation over the
@@ -99,10 +101,16 @@ class PipelineEngine:
         self.first, self.last = self.s == 0, self.s == self.S - 1
         self.prev = ctx.pp_ranks[self.s - 1] if not self.first else None
         self.next = ctx.pp_ranks[self.s + 1] if not self.last else None
-        self.p2p = P2P()
+        # one communicator per direction: activations (s -> s+1) and their grads (s+1 -> s)
+        self.p2p_f = P2P(getattr(ctx, "pp_fwd_group", None))
+        self.p2p_b = P2P(getattr(ctx, "pp_bwd_group", None))
         self.dtype, self.d = act_dtype, hidden_size
         self.device = ctx.device
         self.stats = {"fwd": 0, "bwd": 0}
+        # receive rings: an activation lives until its micro-batch's backward (at most S - s in
+        # flight on stage s) plus the one prefetched ahead; a gradient only until its backward
+        self._xring = _Ring(self.S - self.s + 1, act_dtype, self.device)
+        self._gring = _Ring(2, act_dtype, self.device)
 
     # ---- per-micro-batch compute ----
     def _act_shape(self, mb):
@@ -126,86 +134,93 @@ class PipelineEngine:
         self.stats["bwd"] += 1
         return x.grad if x is not None else None
 
-    # ---- p2p ----
-    def _recv_fwd(self, mb):
-        if self.first:
-            return None
-        x = torch.empty(self._act_shape(mb), dtype=self.dtype, device=self.device)
-        self.p2p.exchange(recvs=[(x, self.prev)])
-        return x.requires_grad_(True)
-
-    def _send_fwd(self, y):
-        if not self.last:
-            self.p2p.exchange(sends=[(y.detach().contiguous(), self.next)])
-
-    def _send_fwd_recv_bwd(self, y, mb):
-        if self.last:
-            return None
-        g = torch.empty(self._act_shape(mb), dtype=self.dtype, device=self.device)
-        self.p2p.exchange(sends=[(y.detach().contiguous(), self.next)], recvs=[(g, self.next)])
-        return g
-
-    def _recv_bwd(self, mb):
-        if self.last:
-            return None
-        g = torch.empty(self._act_shape(mb), dtype=self.dtype, device=self.device)
-        self.p2p.exchange(recvs=[(g, self.next)])
-        return g
-
-    def _send_bwd(self, gx):
-        if not self.first:
-            self.p2p.exchange(sends=[(gx.contiguous(), self.prev)])
-
-    def _send_bwd_recv_fwd(self, gx, mb_next):
-        if self.first:
-            return None
-        x = torch.empty(self._act_shape(mb_next), dtype=self.dtype, device=self.device)
-        self.p2p.exchange(sends=[(gx.contiguous(), self.prev)], recvs=[(x, self.prev)])
-        return x.requires_grad_(True)
-
     # ---- schedule ----
     def train_batch(self, mbs, gscale, micro_step0):
         """1F1B over ``mbs`` (already on device).  Returns the summed loss (last stage) or None.
 
         micro-batch i runs with ``model.micro_step = micro_step0 + i`` on every
-        stage, so dropout masks are identical to the non-pipelined run."""
+        stage, so dropout masks are identical to the non-pipelined run.
+
+        Communication is asynchronous and posted AHEAD of the compute that needs it:
+        the activation of micro-batch i+1 is requested before micro-batch i's forward runs,
+        and the gradient for the next backward before the forward that precedes it, each
+        into a reusable ring buffer.  Sends are fire-and-forget until the end of the step.
+        On RCCL ``Pending.wait()`` only orders the compute stream behind the transfer, so
+        the host never blocks and xGMI transfers overlap the forward / backward kernels."""
         M = len(mbs)
         nwarm = min(self.S - self.s - 1, M)
         nsteady = M - nwarm
         live = deque()
+        xq = deque()
+        sends = []
         loss_acc = torch.zeros((), dtype=torch.float32, device=self.device) if self.last else None
+
+        def post_x(i):
+            if not self.first and i < M:
+                buf = self._xring.get(self._act_shape(mbs[i]))
+                xq.append(self.p2p_f.post(recvs=[(buf, self.prev)]))
+
+        def take_x():
+            if self.first:
+                return None
+            return xq.popleft().wait()[0].requires_grad_(True)
+
+        def post_g(b):
+            if self.last:
+                return None
+            return self.p2p_b.post(recvs=[(self._gring.get(self._act_shape(mbs[b])), self.next)])
 
         def fwd(i, x):
             y = self._forward(mbs[i], x, micro_step0 + i)
             if self.last:
                 loss_acc.add_(y.detach())
+            else:
+                sends.append(self.p2p_f.post(sends=[(y.detach(), self.next)]))
             return y
 
+        def bwd(gp):
+            bx, by = live.popleft()
+            g = gp.wait()[0] if gp is not None else None
+            gx = self._backward(by, bx, g, gscale)
+            if not self.first:
+                sends.append(self.p2p_b.post(sends=[(gx, self.prev)]))
+                bx.grad = None  # the ring slot is reused by a later micro-batch
+
+        post_x(0)
         for i in range(nwarm):
-            x = self._recv_fwd(mbs[i])
-            y = fwd(i, x)
-            self._send_fwd(y)
-            live.append((x, y))
-        x = self._recv_fwd(mbs[nwarm]) if nsteady > 0 else None
+            x = take_x()
+            post_x(i + 1)
+            live.append((x, fwd(i, x)))
         for j in range(nsteady):
             i = nwarm + j
-            y = fwd(i, x)
-            g = self._send_fwd_recv_bwd(y, mbs[i - nwarm])  # grad of the oldest live micro-batch
-            live.append((x, y))
-            bx, by = live.popleft()
-            gx = self._backward(by, bx, g, gscale)
-            if j == nsteady - 1:
-                self._send_bwd(gx)
-                x = None
-            else:
-                x = self._send_bwd_recv_fwd(gx, mbs[i + 1])
+            gp = post_g(j)          # grad of the oldest live micro-batch, requested before the forward
+            x = take_x()
+            post_x(i + 1)
+            live.append((x, fwd(i, x)))
+            bwd(gp)
         for k in range(nwarm):
-            bi = nsteady + k
-            g = self._recv_bwd(mbs[bi])
-            bx, by = live.popleft()
-            gx = self._backward(by, bx, g, gscale)
-            self._send_bwd(gx)
+            bwd(post_g(nsteady + k))
+        for p in sends:
+            p.wait()
         return loss_acc
+
+
+class _Ring:
+    """Receive buffers reused round-robin per shape (``n`` slots: the in-flight bound)."""
+
+    def __init__(self, n, dtype, device):
+        self.n, self.dtype, self.device = max(1, n), dtype, device
+        self.bufs, self.idx = {}, {}
+
+    def get(self, shape):
+        shape = tuple(shape)
+        bufs = self.bufs.setdefault(shape, [])
+        i = self.idx.get(shape, 0)
+        self.idx[shape] = i + 1
+        if len(bufs) < self.n:
+            bufs.append(torch.empty(shape, dtype=self.dtype, device=self.device))
+        # a fresh leaf view per use: no autograd state (.grad, requires_grad) carries over
+        return bufs[i % self.n].detach()
 
 
 def schedule_1f1b(S, s, M):

@@ -99,9 +99,12 @@ class GraphedStep:
         torch.cuda.synchronize()
         graph_seeds(True)
         streams.set_enabled(os.environ.get("MIFT_GRAPH_SIDE", "0") == "1")
+        red = tr.reducer
         try:
-            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
-                self._fwd_bwd(ent, len(mbs))
+            # collectives are never captured: the DP buckets launch after the replay (finish())
+            with (red.no_sync() if red is not None else _nullctx()):
+                with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
+                    self._fwd_bwd(ent, len(mbs))
         finally:
             graph_seeds(False)
             streams.set_enabled(None)
@@ -137,3 +140,11 @@ class GraphedStep:
 def _C():
     from ..ops.dispatch import C
     return C()
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

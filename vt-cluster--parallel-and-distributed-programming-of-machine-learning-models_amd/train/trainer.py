@@ -59,7 +59,7 @@ class TrainConfig:
     zero_stage: int = 0                # 1: shard AdamW state over the DP group (mift.parallel.zero)
     trainable: str = "lora"            # lora | all (full fine-tuning: the tiny-BERT lab)
     logging_first_step: bool = False
-    graph: str = "off"                 # hipGraph-replayed steps (mift.train.graph): on | off (MIFT_GRAPH)
+    graph: str = "auto"                # hipGraph-replayed steps (mift.train.graph): auto | on | off (MIFT_GRAPH)
     consistency_every: int = 0         # >0: checksum the trainable params across DP replicas every N steps
 
 
@@ -141,6 +141,11 @@ class Trainer:
     # ------------------------------------------------------------------
     def _global_tokens(self, mbs):
         count = getattr(self.model, "count_targets", None)
+        pre = getattr(mbs, "global_tokens", None)
+        if count is None and pre is not None:
+            # causal LM: precomputed from the deterministic shard plan (MicroBatcher.global_step_tokens),
+            # so the step issues no blocking control-plane all-reduce
+            return max(int(pre), 1)
         if count is not None:  # e.g. sequence classification: one target per row
             n = sum(count(mb["labels"]) for mb in mbs)
         else:  # causal LM: shifted label tokens
@@ -173,6 +178,8 @@ class Trainer:
         """One optimizer step over a list of micro-batches. Returns loss_sum tensor."""
         model, cfg = self.model, self.cfg
         ntok = self._global_tokens(mbs)
+        if self.reducer is not None:
+            self.reducer.begin_step()
         lr = self.sched(self.global_step)
         self.opt.set_lr(lr)
         if self.graphed is not None and self.graphed.supported(mbs):
@@ -332,8 +339,11 @@ class Trainer:
                            "zero_stage": int(self.zero)}, f, indent=2)
         if dist.is_initialized():
             dist.barrier(group=self.ctx.ctrl_group if self.ctx else None)
-        # optimizer state is per rank in PP (stage-local adapters) and ZeRO-1 (shards)
-        torch.save(self.opt.state_dict(), os.path.join(out, self._opt_file()))
+        os.makedirs(out, exist_ok=True)  # every rank: a rank on another node may not see rank 0's mkdir yet
+        # optimizer state is per rank in PP (stage-local adapters) and ZeRO-1 (shards); plain DDP
+        # replicas hold identical state, so only rank 0 writes the shared optimizer.pt
+        if self._opt_per_rank() or self.rank == 0:
+            torch.save(self.opt.state_dict(), os.path.join(out, self._opt_file()))
         torch.save({"cpu": torch.get_rng_state()}, os.path.join(out, f"rng_state_{self.rank}.pth"))
         if dist.is_initialized():
             dist.barrier(group=self.ctx.ctrl_group if self.ctx else None)
@@ -344,8 +354,11 @@ class Trainer:
                 shutil.rmtree(os.path.join(self.cfg.output_dir, d), ignore_errors=True)
         return out
 
+    def _opt_per_rank(self):
+        return self.pp > 1 or self.zero
+
     def _opt_file(self):
-        return "optimizer.pt" if (self.pp == 1 and not self.zero) else f"optimizer_rank{self.rank}.pt"
+        return f"optimizer_rank{self.rank}.pt" if self._opt_per_rank() else "optimizer.pt"
 
     def adapter_state(self):
         """Full PEFT adapter state (gathered over pipeline stages) on rank 0."""
