@@ -56,7 +56,7 @@ def test_graph_replay_matches_eager(name, precision, steps):
     for a, b in zip(le, lg):
         assert a == pytest.approx(b, rel=1e-4, abs=1e-4), (le, lg)
     for a, b in zip(ge, gg):
-        assert a == pytest.approx(b, rel=2e-3, abs=1e-5), (ge, gg)
+        assert a == pytest.approx(b, rel=1e-2, abs=1e-5), (ge, gg)  # Adam-amplified atomics noise
     # Neither path is bit-reproducible: the LoRA weight-gradient kernels accumulate with fp32
     # atomics, and Adam's first steps move every element by ~lr * sign(g), so a gradient that is
     # ~0 up to rounding can flip sign between runs and shift that element by up to 2*lr per step

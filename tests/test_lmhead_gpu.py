@@ -1,0 +1,96 @@
+"""Fused LM head + cross-entropy (csrc/kernels/gemm.hip EPI 1/2, ops.fused.LMHeadXent) vs a plain
+PyTorch fp32 reference: loss, per-row logsumexp and the gradient w.r.t. the hidden states, for
+both vocab sizes (GPT-2 50257, OPT 50272 padded to 50304), bf16 and fp16, with ignored targets
+(-100 and OPT's pad-id ignore_index), and an upstream gradient that is not 1."""
+import pytest
+import torch
+import torch.nn.functional as TF
+
+import mift
+from mift.ops import fused as F
+from mift.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+class _LN(torch.nn.Module):
+    def __init__(self, d, dtype, dev, g):
+        super().__init__()
+        self.weight = torch.nn.Parameter((1 + 0.1 * torch.randn(d, generator=g, device=dev)).to(dtype),
+                                         requires_grad=False)
+        self.bias = torch.nn.Parameter((0.1 * torch.randn(d, generator=g, device=dev)).to(dtype), requires_grad=False)
+        self.eps = 1e-5
+
+
+def _case(V, dtype, ignore_index, M=1536, d=768, scale=1.0):
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(V + M)
+    Vp = (V + 63) // 64 * 64
+    h = torch.randn(M, d, generator=g, device=dev).to(dtype)
+    ln = _LN(d, dtype, dev, g)
+    W = torch.zeros(Vp, d, device=dev, dtype=dtype)
+    W[:V] = (scale * 0.05 * torch.randn(V, d, generator=g, device=dev)).to(dtype)
+    lab = torch.randint(0, V, (M,), generator=g, device=dev)
+    lab[::7] = ignore_index
+    if ignore_index >= 0:
+        lab[3] = ignore_index
+    return h, ln, W, lab, Vp
+
+
+def _ref(h, ln, W, lab, V, ignore_index, gup):
+    hf = h.float().requires_grad_(True)
+    a = TF.layer_norm(hf, (hf.shape[1],), ln.weight.float(), ln.bias.float(), ln.eps)
+    logits = a @ W[:V].float().t()
+    loss = TF.cross_entropy(logits, lab, ignore_index=ignore_index, reduction="sum")
+    (loss * gup).backward()
+    lse = torch.logsumexp(logits, dim=1)
+    return loss.detach(), hf.grad, lse.detach()
+
+
+@pytest.mark.parametrize("V,dtype,ignore", [(50257, torch.bfloat16, -100), (50272, torch.float16, 1),
+                                            (50257, torch.float16, -100), (50272, torch.bfloat16, 1)])
+def test_fused_lmhead_matches_fp32(V, dtype, ignore):
+    assert mift.kernels_available()
+    h, ln, W, lab, Vp = _case(V, dtype, ignore)
+    gup = 0.37
+    hx = h.clone().requires_grad_(True)
+    loss = F.lm_head_xent(hx, ln, W, lab, V, ignore, need_grad=True, w_kn=W.t().contiguous())
+    (loss * gup).backward()
+    rl, rg, rlse = _ref(h, ln, W, lab, V, ignore, gup)
+    assert float(loss) == pytest.approx(float(rl), rel=3e-3)
+    err = (hx.grad.float() - rg).norm() / rg.norm()
+    assert err < 3e-2, float(err)
+
+
+def test_lmhead_stats_and_lse():
+    """Kernel pieces: E = exp(z - m_tile) <= 1, tile max, per-row lse, label logit."""
+    V, dtype = 50257, torch.bfloat16
+    h, ln, W, lab, Vp = _case(V, dtype, -100, M=512)
+    a, _, _ = K.layer_norm_fwd(h, ln.weight, ln.bias, ln.eps)
+    E, stats, lse, loss, zlab = K.lmhead_fwd(a, W, lab, V)
+    z = a.float() @ W.float().t()
+    zr = z[:, :V]
+    assert E.shape == (512, Vp) and stats.shape == (512, (Vp + 255) // 256, 2)
+    torch.testing.assert_close(lse, torch.logsumexp(zr, 1), atol=2e-2, rtol=1e-3)
+    m_ref = torch.stack([zr[:, j * 256:min(V, (j + 1) * 256)].max(1).values for j in range(stats.shape[1])], 1)
+    torch.testing.assert_close(stats[..., 0], m_ref, atol=2e-2, rtol=1e-3)
+    Ef = E.float()[:, :V]
+    assert float(Ef.max()) <= 1.0 + 1e-3 and float(E.float()[:, V:].abs().max()) == 0.0
+    tm = stats[..., 0].repeat_interleave(256, 1)[:, :V]
+    torch.testing.assert_close(Ef, torch.exp(zr - tm), atol=1e-2, rtol=1e-2)
+    ok = lab >= 0
+    torch.testing.assert_close(zlab[ok], zr[ok].gather(1, lab[ok, None])[:, 0], atol=2e-2, rtol=1e-3)
+    torch.testing.assert_close(loss[~ok], torch.zeros_like(loss[~ok]))
+
+
+def test_lmhead_large_logits_stable():
+    """Peaked rows (|z| ~ 60): tile-relative E keeps every value finite and the loss exact."""
+    V, dtype = 50257, torch.bfloat16
+    h, ln, W, lab, Vp = _case(V, dtype, -100, M=768, scale=6.0)
+    hx = h.clone().requires_grad_(True)
+    loss = F.lm_head_xent(hx, ln, W, lab, V, -100, need_grad=True, w_kn=W.t().contiguous())
+    loss.backward()
+    rl, rg, _ = _ref(h, ln, W, lab, V, -100, 1.0)
+    assert torch.isfinite(hx.grad).all()
+    assert float(loss) == pytest.approx(float(rl), rel=3e-3)
+    assert float((hx.grad.float() - rg).norm() / rg.norm()) < 3e-2

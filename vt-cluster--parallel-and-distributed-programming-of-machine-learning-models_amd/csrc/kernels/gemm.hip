@@ -51,7 +51,31 @@ enum Act : int {
   ACT_GELU_ERF_BWD = 6,
 };
 
+// Fused LM head + cross-entropy (EPI 1 / 2 below; host: mift_lmhead_fwd / mift_lmhead_dgrad).
+//   forward  (EPI 1, phased 256x256 tile): z = x·Wᵀ stays in registers; per (row, 256-column tile j)
+//            the epilogue writes E = exp(z - m_j) (16-bit, <= 1), the tile max m_j and
+//            s_j = Σ_tile E, and the fp32 logit of the row's label.  Logits are never stored.
+//   loss     (lmhead_lse_kernel): lse = log Σ_j s_j·exp(m_j), loss = lse - z_label.
+//   backward (EPI 2, phased 256x256 tile, split-K): dlogits = g·(E·exp(m_j - lse) - onehot)
+//            is never materialised: dX = g·(Σ_j exp(m_j - lse)·E_j·W_j - W[label]); the per-row,
+//            per-column-tile factors are applied flash-attention style, rescaling the
+//            accumulator at every 256-column group boundary; the one-hot part and g are applied
+//            in the split-K reduction (lmhead_reduce_kernel).
+struct LmArgs {
+  const int64_t* labels;  // [M] (ignore_index / out of range -> no target)
+  int V;                  // real vocabulary (columns >= V are padding)
+  float2* stats;          // [M][ntn] (m_j, s_j)
+  float* zlab;            // [M] fp32 logit of the label
+  // backward
+  const float* lse;       // [M]
+  const float* gscale;    // device scalar: upstream grad (x loss scale / tokens)
+  int ntn;                // column tiles of the forward (= groups of the backward)
+  int gpc;                // groups per split-K chunk
+  float* partial;         // [S][M][N] fp32 split-K slabs
+};
+
 struct EpiArgs {
+  LmArgs lm;
   const void* bias;  // [N] (T or float)
   int bias_f32;
   const void* aux;   // [M,N] T (pre-activation for *_BWD)
@@ -111,6 +135,7 @@ MIFT_HD float apply_act(int act, float z, float aux) {
 
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;  // bytes per LDS row (128)
+constexpr int LM_GW = 24;     // LM-head dgrad: groups (forward column tiles) per LDS window of tile maxima
 
 // s_waitcnt vmcnt(n) with a compile-time n (0..63)
 template <int N>
@@ -119,7 +144,7 @@ MIFT_HD void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, bool SKM>
+template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, bool SKM, int EPI = 0>
 __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                                 T* __restrict__ C, const T* __restrict__ A2,
                                                                 const T* __restrict__ B2, int M, int N, int K,
@@ -236,14 +261,11 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   // Buffer hazards (two buffers, tile t in buffer t&1): a region is restaged >= 2 phases after
   // its last ds_read (B of tile kt read last in ph1 -> B(kt+2) in ph3; A of tile kt-1 read last
   // in its ph2 -> A(kt+1) in ph0/ph1), and read >= 1 phase after the wait that retires it.
-  auto mainloop8 = [&]() {
+  // acc += sum over k-tiles [kb, ke); hook(kt) runs at the top of every k-tile (before its reads)
+  auto mainloop8 = [&](int kb, int ke, auto&& hook) {
    if constexpr (NSTAGE == 0) {
     static_assert(BM == 256 && BN == 256 && NWM == 2 && NWN == 4, "phased loop: 256x256 tile, 2x4 waves");
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
-    const int nk = K / BK;
+    const int nk = ke - kb;
     // half h (rows 128h..128h+127) of operand o (0 = A, 1 = B) of k-tile t -> buffer t & 1
     auto stage_half = [&](int t, int o, int h) {
       char* base = smem + (t & 1) * STAGE_BYTES + o * A_BYTES;
@@ -256,7 +278,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         const int i = 16 * h + wave + 8 * ii;
         const int r = i * 8 + srow;
         const int gr = min(r00 + r, rmax);
-        __builtin_amdgcn_global_load_lds((const void*)(G + (size_t)gr * ld + t * BK + (spc ^ (r & 7)) * 8),
+        __builtin_amdgcn_global_load_lds((const void*)(G + (size_t)gr * ld + (kb + t) * BK + (spc ^ (r & 7)) * 8),
                                          (void*)(base + i * 1024), 16, 0, 0);
       }
     };
@@ -296,6 +318,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
     asm volatile("" ::: "memory");
     for (int kt = 0; kt < nk; ++kt) {
+      hook(kt);
       const char* As = smem + (kt & 1) * STAGE_BYTES;
       const char* Bs = As + A_BYTES;
       // ph0
@@ -507,8 +530,158 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     }
   };
 
+  // ---- EPI 1: LM-head forward epilogue (see LmArgs) — registers only, the ring is reused for
+  // two [NW][WM] row-partial arrays (max, sum) exchanged between the NWN waves of a row.
+  auto lm_fwd_epilogue = [&]() {
+    const LmArgs& lm = ep.lm;
+    __syncthreads();  // every wave is done reading the staging ring
+    float* redm = reinterpret_cast<float*>(smem);
+    float* reds = redm + NW * WM;
+    const int V = lm.V;
+    constexpr float L2E = 1.4426950408889634f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 16 + fq * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = (col + e < V) ? fmaxf(m, acc[i][j][e]) : m;
+      }
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      if (fq == 0) redm[wave * WM + i * 16 + fr] = m;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < NWN; ++w) m = fmaxf(m, redm[(wm * NWN + w) * WM + i * 16 + fr]);
+      if (m == -INFINITY) m = 0.f;  // tile entirely beyond V (cannot happen for V_pad - V < BN)
+      const int row = m0 + wm * WM + i * 16 + fr;
+      const bool rok = row < M;
+      const int64_t lab = rok ? lm.labels[row] : -1;
+      const float mb = m * L2E;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 16 + fq * 4;
+        float ev[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ev[e] = (col + e < V) ? __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][e], L2E, -mb)) : 0.f;
+          s += ev[e];
+        }
+        const int64_t d = lab - col;
+        if (d >= 0 && d < 4 && lab < V) {  // static selects: a runtime vector index would go to scratch
+          const float4_ a = acc[i][j];
+          lm.zlab[row] = d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
+        }
+        if (rok && col < N) store4<T>(C + (size_t)row * ldc + col, ev);
+      }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (fq == 0) reds[wave * WM + i * 16 + fr] = s;
+    }
+    __syncthreads();
+    if (tid < BM) {  // one thread per block row: combine the NWN wave partials
+      const int wr = tid / WM, rr = tid % WM;
+      const int row = m0 + tid;
+      float m = -INFINITY, s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWN; ++w) {
+        m = fmaxf(m, redm[(wr * NWN + w) * WM + rr]);
+        s += reds[(wr * NWN + w) * WM + rr];
+      }
+      if (m == -INFINITY) m = 0.f;
+      if (row < M) lm.stats[(size_t)row * lm.ntn + n0 / BN] = make_float2(m, s);
+    }
+  };
+
   const int nk_all = K / BK;
-  if constexpr (!SKM) {
+  if constexpr (EPI == 1) {
+    static_assert(NSTAGE == 0, "LM-head forward runs on the phased 256x256 tile");
+    const int nblk = gridDim.x;
+    int bid = blockIdx.x;
+    {
+      const int q = nblk / 8, r = nblk % 8;
+      const int xcd = bid % 8, loc = bid / 8;
+      bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    }
+    m0 = (bid / ntn) * BM;
+    n0 = (bid % ntn) * BN;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+    mainloop8(0, nk_all, [](int) {});
+    lm_fwd_epilogue();
+    return;
+  } else if constexpr (EPI == 2) {
+    // ---- LM-head dgrad on the phased 256x256 tile.  A = E [M, V_pad], B = Wᵀ [N, V_pad].
+    // Each group of GK k-tiles is one forward column tile j whose E is relative to its own max
+    // m_j.  Flash-style, acc is kept relative to a per-row reference ref: at every group start
+    // acc *= exp(ref - ref'), ref' = max(m_j, ref - 60) (the clamp bounds acc's growth by e^60;
+    // a tile more than 60 below the running reference contributes < e^-60 of the row, so adding
+    // it at the clamped reference errs by < e^-60 relative), and the chunk's result is
+    // acc·exp(ref - lse).  Block -> (tile, split-K chunk of gpc groups); the reduction kernel
+    // sums the chunks, subtracts W[label] and applies the upstream gradient.
+    static_assert(NSTAGE == 0, "LM-head dgrad runs on the phased 256x256 tile");
+    const LmArgs& lm = ep.lm;
+    const int S = (lm.ntn + lm.gpc - 1) / lm.gpc;
+    const int tl = blockIdx.x / S, cidx = blockIdx.x % S;
+    m0 = (tl / ntn) * BM;
+    n0 = (tl % ntn) * BN;
+    const int g0 = cidx * lm.gpc, g1 = min(lm.ntn, g0 + lm.gpc);
+    constexpr int GK = 256 / BK;
+    constexpr int cstride = LM_GW | 1;  // odd stride: the 16 rows of a fragment hit 16 banks
+    float* ms = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);  // [BM][cstride] tile maxima, behind the ring
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+    float ref[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) ref[i] = -INFINITY;
+    for (int w0 = g0; w0 < g1; w0 += LM_GW) {
+      const int w1 = min(g1, w0 + LM_GW), nw = w1 - w0;
+      __syncthreads();  // the previous window's readers are done
+      for (int x = tid; x < BM * nw; x += NT) {
+        const int r = x / nw, g = x % nw;
+        const int row = min(m0 + r, M - 1);
+        ms[r * cstride + g] = lm.stats[(size_t)row * lm.ntn + w0 + g].x;
+      }
+      __syncthreads();
+      mainloop8(w0 * GK, min(nk_all, w1 * GK), [&](int kt) {
+        const int gk = w0 * GK + kt;
+        if (gk % GK != 0) return;
+        const int g = gk / GK - w0;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float m = ms[(wm * WM + i * 16 + fr) * cstride + g];
+          const float rn = fmaxf(m, ref[i] - 60.f);
+          const float f = __expf(ref[i] - rn);  // 0 on the first group (acc is 0 there)
+          ref[i] = rn;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] *= f;
+        }
+      });
+    }
+    float* dst = lm.partial + (size_t)cidx * M * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = m0 + wm * WM + i * 16 + fr;
+      if (row >= M) continue;
+      const float fac = __expf(ref[i] - lm.lse[row]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 16 + fq * 4;
+        if (col < N) *reinterpret_cast<float4_*>(dst + (size_t)row * N + col) = acc[i][j] * fac;
+      }
+    }
+    return;
+  } else if constexpr (!SKM) {
     // ---- data-parallel tile, XCD-aware bijective block remap (T1) ----
     const int nblk = gridDim.x;  // tiles [0, gridDim.x) (all of them unless stream-K takes the tail)
     int bid = blockIdx.x;
@@ -519,8 +692,15 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     }
     m0 = (bid / ntn) * BM;
     n0 = (bid % ntn) * BN;
-    if constexpr (NSTAGE == 0) mainloop8();
-    else mainloop(0, nk_all);
+    if constexpr (NSTAGE == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+      mainloop8(0, nk_all, [](int) {});
+    } else {
+      mainloop(0, nk_all);
+    }
     epilogue();
     return;
   } else {
@@ -702,7 +882,184 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
   }
 }
 
+// ---- LM head: loss from the forward's tile statistics (one wave per row) ----
+__global__ __launch_bounds__(256) void lmhead_lse_kernel(const float2* __restrict__ stats, int ntn,
+                                                         const float* __restrict__ zlab,
+                                                         const int64_t* __restrict__ labels, int V, int M,
+                                                         float* __restrict__ lse, float* __restrict__ loss) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float2* st = stats + (size_t)row * ntn;
+  float m = -INFINITY;
+  for (int j = lane; j < ntn; j += 64) m = fmaxf(m, st[j].x);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int j = lane; j < ntn; j += 64) s += st[j].y * __expf(st[j].x - m);
+  s = wave_sum(s);
+  if (lane == 0) {
+    const float l = m + __logf(s);
+    lse[row] = l;
+    const int64_t lab = labels[row];
+    loss[row] = (lab >= 0 && lab < V) ? l - zlab[row] : 0.f;
+  }
+}
+
+// ---- LM head: sum the split-K slabs, subtract g·W[label] (the one-hot part of dlogits) ----
+template <typename T>
+__global__ __launch_bounds__(256) void lmhead_reduce_kernel(const float* __restrict__ partial, int S, int M, int N,
+                                                            const T* __restrict__ w, int ldw,
+                                                            const int64_t* __restrict__ labels, int V,
+                                                            const float* __restrict__ gscale, T* __restrict__ out) {
+  const size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;  // one 8-column chunk
+  const int cpr = N / 8;
+  if (v >= (size_t)M * cpr) return;
+  const int row = (int)(v / cpr), c8 = (int)(v % cpr) * 8;
+  float acc[8];
+  {
+    const float4* p = reinterpret_cast<const float4*>(partial + (size_t)row * N + c8);
+    float4 a = p[0], b = p[1];
+    acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w; acc[4] = b.x; acc[5] = b.y; acc[6] = b.z; acc[7] = b.w;
+  }
+  for (int s = 1; s < S; ++s) {
+    const float4* p = reinterpret_cast<const float4*>(partial + ((size_t)s * M + row) * N + c8);
+    float4 a = p[0], b = p[1];
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w; acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+  }
+  const int64_t lab = labels[row];
+  if (lab >= 0 && lab < V) {  // dX = g·(softmax·W - W[label]); rows without a target get 0
+    float wv[8];
+    load8<T>(w + (size_t)lab * ldw + c8, wv);
+    const float g = gscale[0];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = g * (acc[e] - wv[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  }
+  store8<T>(out + (size_t)row * N + c8, acc);
+}
+
+template <typename T>
+std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int V) {
+  const int M = a.size(0), K = a.size(1), N = w.size(0);
+  constexpr int BM = 256, BN = 256;
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
+  auto E = at::empty({M, N}, a.options());
+  auto f32 = a.options().dtype(at::kFloat);
+  auto stats = at::empty({M, ntn, 2}, f32);
+  auto zlab = at::zeros({M}, f32);
+  auto lse = at::empty({M}, f32);
+  auto loss = at::empty({M}, f32);
+  EpiArgs ep{};
+  ep.alpha = 1.f;
+  ep.lm.labels = labels.data_ptr<int64_t>();
+  ep.lm.V = V;
+  ep.lm.stats = reinterpret_cast<float2*>(stats.data_ptr<float>());
+  ep.lm.zlab = zlab.data_ptr<float>();
+  ep.lm.ntn = ntn;
+  SkArgs sk{};
+  constexpr int SMEM = 2 * (BM + BN) * ROWB;
+  auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr = true;
+  }
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  hipLaunchKernelGGL(kern, dim3(ntm * ntn), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
+                     (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
+  hipLaunchKernelGGL(lmhead_lse_kernel, dim3((M + 3) / 4), dim3(256), 0, st,
+                     reinterpret_cast<const float2*>(stats.data_ptr<float>()), ntn, zlab.data_ptr<float>(),
+                     labels.data_ptr<int64_t>(), V, M, lse.data_ptr<float>(), loss.data_ptr<float>());
+  return {E, stats, lse, loss, zlab};
+}
+
+template <typename T>
+at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
+                             int V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale) {
+  const int M = E.size(0), K = E.size(1), N = wt.size(0);
+  const int ntn_f = stats.size(1);
+  constexpr int BM = 256, BN = 256;
+  constexpr int STAGE_BYTES = (BM + BN) * ROWB;
+  constexpr int SMEM = 2 * STAGE_BYTES + BM * (LM_GW | 1) * 4;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  // split the vocabulary so the grid is a whole number of chip waves (one block per CU), >= 3 waves
+  const int cus = num_cus();
+  int S = std::max(1, std::min(ntn_f, (3 * cus + tiles - 1) / tiles));
+  const int gpc = (ntn_f + S - 1) / S;
+  S = (ntn_f + gpc - 1) / gpc;
+  auto partial = at::empty({S, M, N}, E.options().dtype(at::kFloat));
+  EpiArgs ep{};
+  ep.alpha = 1.f;
+  ep.lm.labels = labels.data_ptr<int64_t>();
+  ep.lm.V = V;
+  ep.lm.stats = reinterpret_cast<float2*>(const_cast<float*>(stats.data_ptr<float>()));
+  ep.lm.lse = lse.data_ptr<float>();
+  ep.lm.gscale = gscale.data_ptr<float>();
+  ep.lm.ntn = ntn_f;
+  ep.lm.gpc = gpc;
+  ep.lm.partial = partial.data_ptr<float>();
+  SkArgs sk{};
+  auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr = true;
+  }
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  hipLaunchKernelGGL(kern, dim3(tiles * S), dim3(512), SMEM, st, (const T*)E.data_ptr(), (const T*)wt.data_ptr(),
+                     (T*)nullptr, nullptr, nullptr, M, N, K, (int)E.stride(0), (int)wt.stride(0), N, ep, sk);
+  auto out = at::empty({M, N}, E.options());
+  const size_t chunks = (size_t)M * (N / 8);
+  hipLaunchKernelGGL(lmhead_reduce_kernel<T>, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st,
+                     partial.data_ptr<float>(), S, M, N, (const T*)w.data_ptr(), (int)w.stride(0),
+                     labels.data_ptr<int64_t>(), V, gscale.data_ptr<float>(), (T*)out.data_ptr());
+  return out;
+}
+
 }  // namespace
+
+// Fused LM head + cross-entropy forward: a = LN(h) [M,K], w = tied embedding [V_pad,K],
+// labels [M] int64 (already shifted; ignore -> any value outside [0, V)).
+// -> (E [M,V_pad] = exp(z - m_tile) 16-bit, stats [M, V_pad/256, 2] (m, s), lse [M], loss [M], zlab [M]).
+std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V) {
+  TORCH_CHECK(a.is_cuda() && w.is_cuda() && labels.is_cuda(), "lmhead_fwd: GPU tensors");
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1), "lmhead_fwd: a [M,K], w [V_pad,K]");
+  TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && a.size(1) % 64 == 0, "lmhead_fwd: K-contiguous, K % 64 == 0");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "lmhead_fwd: 16-B aligned rows");
+  TORCH_CHECK(w.size(0) % 4 == 0 && V <= w.size(0) && w.size(0) - V < 256, "lmhead_fwd: V_pad % 4, V_pad - V < 256");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == a.size(0),
+              "lmhead_fwd: int64 labels [M]");
+  TORCH_CHECK(a.scalar_type() == w.scalar_type(), "lmhead_fwd: dtype mismatch");
+  if (a.scalar_type() == at::kBFloat16) return lmhead_fwd_impl<bf16>(a, w, labels, (int)V);
+  TORCH_CHECK(a.scalar_type() == at::kHalf, "lmhead_fwd: bf16/fp16");
+  return lmhead_fwd_impl<fp16>(a, w, labels, (int)V);
+}
+
+// Backward of the fused head: dX [M,N] = g·(softmax - onehot)·W without materialising dlogits.
+// E / stats / lse from mift_lmhead_fwd; wt = Wᵀ [N, V_pad] (K-contiguous), w = W [V_pad, N];
+// gscale: 1-element fp32 device tensor (upstream gradient, e.g. loss_scale / tokens).
+at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
+                             int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale) {
+  TORCH_CHECK(E.is_cuda() && wt.is_cuda() && w.is_cuda(), "lmhead_dgrad: GPU tensors");
+  TORCH_CHECK(E.dim() == 2 && wt.dim() == 2 && wt.size(1) == E.size(1), "lmhead_dgrad: E [M,V_pad], wt [N,V_pad]");
+  TORCH_CHECK(E.stride(1) == 1 && wt.stride(1) == 1 && E.size(1) % 64 == 0, "lmhead_dgrad: V_pad % 64 == 0");
+  TORCH_CHECK(E.is_contiguous() && wt.stride(0) % 8 == 0, "lmhead_dgrad: layouts");
+  TORCH_CHECK(w.size(0) >= V && w.size(1) == wt.size(0) && w.stride(1) == 1 && w.stride(0) % 8 == 0,
+              "lmhead_dgrad: w [V_pad, N]");
+  TORCH_CHECK(wt.size(0) % 8 == 0, "lmhead_dgrad: N % 8 == 0");
+  TORCH_CHECK(stats.dim() == 3 && stats.size(0) == E.size(0) && stats.size(2) == 2 && stats.is_contiguous() &&
+                  stats.size(1) * 256 >= E.size(1),
+              "lmhead_dgrad: stats [M, ntn, 2]");
+  TORCH_CHECK(lse.numel() == E.size(0) && gscale.numel() >= 1 && gscale.scalar_type() == at::kFloat,
+              "lmhead_dgrad: lse [M], fp32 gscale");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == E.size(0), "lmhead_dgrad: labels");
+  if (E.scalar_type() == at::kBFloat16) return lmhead_dgrad_impl<bf16>(E, wt, w, labels, (int)V, stats, lse, gscale);
+  TORCH_CHECK(E.scalar_type() == at::kHalf, "lmhead_dgrad: bf16/fp16");
+  return lmhead_dgrad_impl<fp16>(E, wt, w, labels, (int)V, stats, lse, gscale);
+}
 
 // out = epi(a @ b^T [+ a2 @ b2^T]).  a:[M,K], b:[N,K] (K-contiguous, K%64==0).
 std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,

@@ -20,6 +20,11 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                                      int64_t tile, const c10::optional<at::Tensor>& alpha_t,
                                      const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed);
 
+// ---- K2/K7 fused LM head + cross-entropy (kernels/gemm.hip, EPI 1/2)
+std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V);
+at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
+                             int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale);
+
 // ---- LoRA side path (kernels/lora.hip)
 at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed);
 void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, double p, int64_t seed, int64_t mode,
@@ -75,6 +80,8 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
   m.def("attn_fwd", &mift_attn_fwd, "causal flash attention fwd on fused qkv -> (o, lse)"); \
   m.def("attn_bwd", &mift_attn_bwd, "causal flash attention bwd -> dqkv"); \
   m.def("gemm_nt", &mift_gemm_nt, "C = epi(A @ B^T [+ A2 @ B2^T]) MFMA bf16/fp16"); \
+  m.def("lmhead_fwd", &mift_lmhead_fwd, "fused LM head + CE fwd -> (E, stats, lse, loss, zlab)"); \
+  m.def("lmhead_dgrad", &mift_lmhead_dgrad, "fused LM head + CE dgrad -> dX (no dlogits)"); \
   m.def("grad_stats", &mift_grad_stats, "sum(g^2), nonfinite count -> stats[2]"); \
   m.def("opt_finalize", &mift_opt_finalize, "clip coef / found_inf / step / loss-scale update"); \
   m.def("adamw", &mift_adamw, "fused AdamW over a flat fp32 arena (zeroes grads)"); \

@@ -32,14 +32,19 @@ class CausalLMBase(nn.Module):
 
     # subclasses: tied_embedding() -> nn.Parameter [V, d]; blocks() -> list
 
-    def lm_weight_padded(self):
-        """Tied LM head as ([V_pad, d], [d, V_pad]) with zero rows beyond the vocab."""
+    def lm_weight_padded(self, transposed=False):
+        """Tied LM head as ([V_pad, d], [d, V_pad] or None) with zero rows beyond the vocab.
+
+        The [d, V_pad] copy (K-contiguous B operand of the fused head's dgrad, ops/fused.py) is
+        built on first request and cached with the padded weight (frozen: built once)."""
         w = self.tied_embedding()
         key = (w.data_ptr(), w.dtype, w.device)
         if self._head_cache is None or self._head_cache[0] != key:
             wp = torch.zeros(self.vocab_padded, w.shape[1], dtype=w.dtype, device=w.device)
             wp[: w.shape[0]].copy_(w.detach())
             self._head_cache = (key, wp, None)
+        if transposed and self._head_cache[2] is None:
+            self._head_cache = (key, self._head_cache[1], self._head_cache[1].t().contiguous())
         return self._head_cache[1], self._head_cache[2]
 
     def next_micro_step(self):

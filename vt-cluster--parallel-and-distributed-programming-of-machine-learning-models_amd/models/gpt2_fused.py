@@ -37,11 +37,11 @@ def fused_forward(model, input_ids, attention_mask, labels, hidden_states, reduc
             h = blk.forward_fused(h, seeds, training)
     if not model.has_head:
         return {"hidden_states": h}
-    w_nk, _ = model.lm_weight_padded()
+    w_nk, w_kn = model.lm_weight_padded(transposed=labels is not None and torch.is_grad_enabled())
     if labels is not None:
         sl = shift_labels(labels)
         loss_sum = F.lm_head_xent(h, model.transformer.ln_f, w_nk, sl, cfg.vocab_size, -100,
-                                  need_grad=torch.is_grad_enabled())
+                                  need_grad=torch.is_grad_enabled(), w_kn=w_kn)
         ntok = (sl != -100).sum()
         loss = loss_sum / ntok.clamp(min=1) if reduction == "mean" else loss_sum
         return {"loss": loss, "logits": None, "ntokens": ntok}

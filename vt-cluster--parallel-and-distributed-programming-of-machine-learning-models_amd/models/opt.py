@@ -291,11 +291,11 @@ class OPTForCausalLM(CausalLMBase):
                 h = blk.forward_fused(h, seeds, training, kv_len)
         if not self.has_head:
             return {"hidden_states": h}
-        w_nk, _ = self.lm_weight_padded()
+        w_nk, w_kn = self.lm_weight_padded(transposed=labels is not None and torch.is_grad_enabled())
         if labels is not None:
             sl = shift_labels(labels, ignore_index)
             loss_sum = F.lm_head_xent(h, dec.final_layer_norm, w_nk, sl, cfg.vocab_size, ignore_index,
-                                      need_grad=torch.is_grad_enabled())
+                                      need_grad=torch.is_grad_enabled(), w_kn=w_kn)
             ntok = (sl != ignore_index).sum()
             loss = loss_sum / ntok.clamp(min=1) if reduction == "mean" else loss_sum
             return {"loss": loss, "logits": None, "ntokens": ntok}

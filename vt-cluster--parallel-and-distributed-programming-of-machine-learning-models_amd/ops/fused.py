@@ -335,11 +335,46 @@ def mlp(h, ln, fc1, fc2, act, p, seed, seed_l1=0, seed_l2=0, training=True):
 
 # ---------------------------------------------------------------------------
 class LMHeadXent(torch.autograd.Function):
-    """Sum of token CE of LN(h) @ E^T against (already shifted) labels.
+    """Sum of token CE of LN(h) @ E^T against (already shifted) labels — the fused head.
 
-    Forward computes logits into a [M, V_pad] buffer (plain library GEMM:
-    hipBLASLt) and the xent kernel turns it into dlogits in place;
-    backward is one dgrad GEMM scaled by the upstream gradient."""
+    Forward (``lmhead_fwd``, csrc/kernels/gemm.hip EPI 1): the phased 256x256 MFMA GEMM keeps the
+    logits in registers and writes E = exp(z - m_tile) per 256-column tile plus the tile
+    statistics; the loss comes from those statistics (``lmhead_lse_kernel``).  Backward
+    (``lmhead_dgrad``, EPI 2): dX = g·(softmax - onehot)·W as a split-K GEMM over E whose
+    per-row, per-tile factors g·exp(m_tile - lse) are applied to group accumulators, the
+    one-hot part subtracted in the split-K reduction — dlogits are never materialised, the
+    upstream gradient is applied in fp32.  Reference loss head:
+    ``Cluster/Project 2 - Course Project/finetune_lora_opt_pp.py:138-153``.
+
+    ``MIFT_LMHEAD=blas`` selects the previous library path (hipBLASLt logits + xent kernel +
+    hipBLASLt dgrad) for A/B measurements."""
+
+    @staticmethod
+    def forward(ctx, h, ln_w, ln_b, eps, w_nk, labels, V, ignore_index, need_grad, w_kn):
+        shp = h.shape
+        h2 = _flat(h.contiguous())
+        a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
+        lab = labels.reshape(-1)
+        if ignore_index >= 0:  # e.g. OPT ignores the pad id, a real vocabulary entry
+            lab = torch.where(lab == ignore_index, torch.full_like(lab, -1), lab)
+        lab = lab.contiguous()
+        E, stats, lse, loss_rows, _ = K.lmhead_fwd(a, w_nk, lab, V)
+        if need_grad:
+            ctx.save_for_backward(h2, mean, rstd, ln_w, E, stats, lse, lab)
+        ctx.shp, ctx.w_nk, ctx.w_kn, ctx.V = shp, w_nk, w_kn, V
+        return loss_rows.sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        h2, mean, rstd, ln_w, E, stats, lse, lab = ctx.saved_tensors
+        w_kn = ctx.w_kn if ctx.w_kn is not None else ctx.w_nk.t().contiguous()
+        da = K.lmhead_dgrad(E, w_kn, ctx.w_nk, lab, ctx.V, stats, lse, g.reshape(1).float())
+        dh, _, _, _ = K.layer_norm_bwd(da, h2, ln_w, mean, rstd)
+        return dh.view(ctx.shp), None, None, None, None, None, None, None, None, None
+
+
+class LMHeadXentBlas(torch.autograd.Function):
+    """Library path (hipBLASLt logits, xent kernel rewrites them as dlogits, hipBLASLt dgrad)."""
 
     @staticmethod
     def forward(ctx, h, ln_w, ln_b, eps, w_nk, labels, V, ignore_index, need_grad):
@@ -353,9 +388,6 @@ class LMHeadXent(torch.autograd.Function):
             logits = torch.matmul(a, w_nk.t())
             loss_rows, _ = K.xent(logits, lab, V, ignore_index, write_grad=need_grad)
         else:
-            # row chunks: a chunk of logits (chunk x V_pad 16-bit) can stay resident in the 256 MB
-            # Infinity Cache between the GEMM that writes it and the xent kernel that overwrites it
-            # with dlogits (csrc/kernels/xent.hip)
             logits = torch.empty(M, w_nk.shape[0], dtype=a.dtype, device=a.device)
             loss_rows = torch.empty(M, dtype=torch.float32, device=a.device)
             for r0 in range(0, M, chunk):
@@ -371,7 +403,8 @@ class LMHeadXent(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         h2, mean, rstd, ln_w, dlogits = ctx.saved_tensors
-        da = torch.matmul(dlogits, ctx.w_nk).mul_(g.reshape(1).to(dlogits.dtype))
+        da = torch.matmul(dlogits, ctx.w_nk)
+        da = (da.float() * g.reshape(1).float()).to(dlogits.dtype)  # upstream grad applied in fp32
         dh, _, _, _ = K.layer_norm_bwd(da, h2, ln_w, mean, rstd)
         return dh.view(ctx.shp), None, None, None, None, None, None, None, None
 
@@ -388,8 +421,10 @@ def _xent_chunk(M, Vp):
     return M if c <= 0 or c >= M else c
 
 
-def lm_head_xent(h, ln, w_nk, labels, V, ignore_index=-100, need_grad=True):
-    return LMHeadXent.apply(h, ln.weight, ln.bias, ln.eps, w_nk, labels, V, ignore_index, need_grad)
+def lm_head_xent(h, ln, w_nk, labels, V, ignore_index=-100, need_grad=True, w_kn=None):
+    if os.environ.get("MIFT_LMHEAD", "fused") == "blas":
+        return LMHeadXentBlas.apply(h, ln.weight, ln.bias, ln.eps, w_nk, labels, V, ignore_index, need_grad)
+    return LMHeadXent.apply(h, ln.weight, ln.bias, ln.eps, w_nk, labels, V, ignore_index, need_grad, w_kn)
 
 
 def lm_head_logits(h, ln, w_nk, V):

@@ -79,6 +79,16 @@ def pack_lora(A, B, a_scale, dtype):
     return C().pack_lora(A, B, float(a_scale), dtype)
 
 
+def lmhead_fwd(a, w_nk, labels, V):
+    """Fused LM head + CE forward -> (E, stats, lse, loss_rows, zlab); labels outside [0, V) ignored."""
+    return C().lmhead_fwd(a, w_nk, labels, int(V))
+
+
+def lmhead_dgrad(E, w_kn, w_nk, labels, V, stats, lse, gscale):
+    """dX = g·(softmax - onehot)·W from the forward's E / tile stats (no dlogits)."""
+    return C().lmhead_dgrad(E, w_kn, w_nk, labels, int(V), stats, lse, gscale)
+
+
 def xent(logits, labels, V, ignore_index=-100, write_grad=True):
     return C().xent_fwd_bwd(logits, labels, int(V), int(ignore_index), bool(write_grad))
 

@@ -207,7 +207,10 @@ class Trainer:
                 (loss_sum * gscale).backward()
             loss_acc += loss_sum.detach()
             maybe_inject(self.rank, self.global_step + 1, "micro")
-        return self._finish_step(loss_acc, ntok)
+        res = self._finish_step(loss_acc, ntok)
+        if self.graphed is not None:
+            self.graphed.prepare(mbs)  # capture now: the next step of this shape replays
+        return res
 
     def _finish_step(self, loss_acc, ntok):
         self.arena.rebind_grads()
