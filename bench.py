@@ -13,7 +13,10 @@ fused AdamW).  Weak scaling: every rank processes 32 x 256 tokens per step.
   python bench.py --gpus N --steps K --warmup W
   (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
-Prints ONE JSON line on rank 0.  `value` = whole-job tokens/s.
+Prints ONE JSON line on rank 0.  `value` = whole-job steady-state tokens/s over the K timed
+steps; ``wall_clock_epoch_s`` = one full epoch over a 20k-line medium_openwebtext-shaped
+corpus (the reference's other metric, strong-scaled over the DP ranks), run after the timed
+steps.
 """
 import argparse
 import json
@@ -42,6 +45,10 @@ def main():
     ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
                     help="fused = mift HIP kernels; torch = eager PyTorch ops on the same model (comparison)")
     ap.add_argument("--profile_dir", default=None, help="torch.profiler chrome trace of 3 steps")
+    ap.add_argument("--epoch_lines", type=int, default=None,
+                    help="after the timed steps, run one full epoch over this many medium_openwebtext-shaped "
+                         "lines (README.md:66: ~20k) sharded over the DP ranks and report its wall clock "
+                         "(the reference's [Training] sec metric); default 20000 for GPT-2, 0 (skip) for OPT")
     a = ap.parse_args()
     # RCCL / Gloo print their init banners on fd 1 from native code; route
     # everything but the result line to stderr so stdout is exactly ONE JSON line.
@@ -65,6 +72,8 @@ def main():
     a.seq_len = a.seq_len or (512 if is_opt else 256)
     a.accum = a.accum or (96 if is_opt else 32)
     a.precision = a.precision or ("fp16" if is_opt else "bf16")
+    if a.epoch_lines is None:
+        a.epoch_lines = 0 if is_opt else 20000
     ctx = D.init(pp=a.pp, verbose=False, sanity=True)
     if a.gpus != ctx.world:
         if ctx.rank == 0:
@@ -142,11 +151,34 @@ def main():
         prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
         with open(os.path.join(a.profile_dir, "table.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
+    epoch_s, epoch_steps = None, None
+    if a.epoch_lines > 0:
+        # wall-clock/epoch, the other half of the BASELINE metric (reference: max over ranks of
+        # `[Training] x sec`, P1/summarize_medium_times.py:4-10): a fresh epoch over the medium-shaped
+        # corpus, strong-scaled over the DP ranks like the reference's fixed dataset at N nodes
+        eds = synthetic_openwebtext(a.epoch_lines, a.seq_len, model.config.vocab_size, model.config.pad_token_id,
+                                    seed=4321, full_length=True)
+        eb = MicroBatcher(eds, mb, acc, rank=ctx.dp_rank, world=ctx.dp)
+        ep_steps = list(eb.epoch(0))
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        te = time.perf_counter()
+        for s in ep_steps:
+            tr.train_step(s)
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        t = torch.tensor([time.perf_counter() - te], dtype=torch.float64, device=ctx.device)
+        if dist.is_initialized() and n > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        epoch_s, epoch_steps = round(t.item(), 4), len(ep_steps)
     par = f"dp{ctx.dp}" + (f"xpp{ctx.pp}" if ctx.pp > 1 else "") + ("+zero1" if a.zero and ctx.dp > 1 else "")
     if ctx.rank == 0:
         kind = "PP" if ctx.pp > 1 else "DDP"
         out = {
-            "metric": f"{a.model.split('/')[-1]} LoRA {kind} fine-tune throughput (tokens/sec, whole job)",
+            "metric": f"{a.model.split('/')[-1]} LoRA {kind} fine-tune throughput (tokens/sec, whole job, "
+                      f"steady state)",
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": n,
@@ -163,6 +195,10 @@ def main():
                        "split": split, "lora": "r8/a16/p0.05 " + ",".join(targets), "impl": a.impl,
                        "tokens_per_gpu_per_s": round(value / n, 1),
                        "final_grad_norm": round(stats["grad_norm"], 4)},
+            "wall_clock_epoch_s": epoch_s,
+            "epoch": {"lines": a.epoch_lines, "steps": epoch_steps, "global_batch": per_rank * ctx.dp,
+                      "definition": "one pass over the medium-shaped corpus, max over ranks (reference [Training] sec)"}
+            if epoch_s is not None else None,
         }
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())

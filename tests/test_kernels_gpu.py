@@ -178,6 +178,30 @@ def test_flash_attention_fwd_bwd(hd, S, p, dt):
         assert err < 3e-2, f"d{name} rel err {err:.3e}"
 
 
+@pytest.mark.parametrize("S", [256, 200])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_flash_attention_whole_sequence_kernels(S, p, dt, monkeypatch):
+    """The whole-sequence-in-LDS kernels (MIFT_ATTN_SEQ=2 forces them at this small head count)
+    against the fp32 reference, and bit-for-bit agreement of fwd with the tiled kernel."""
+    monkeypatch.setenv("MIFT_ATTN_SEQ", "2")
+    test_flash_attention_fwd_bwd(64, S, p, dt)
+    C = _C()
+    B, H, hd = 2, 3, 64
+    qkv = torch.randn(B * S, 3 * H * hd, device="cuda").to(dt)
+    kvl = torch.tensor([S - 37, S // 3], device="cuda", dtype=torch.int32)
+    o_seq, lse_seq = C.attn_fwd(qkv, B, S, H, hd, hd ** -0.5, p, 99, kvl)
+    monkeypatch.setenv("MIFT_ATTN_SEQ", "0")
+    o_til, lse_til = C.attn_fwd(qkv, B, S, H, hd, hd ** -0.5, p, 99, kvl)
+    torch.testing.assert_close(o_seq, o_til, atol=0, rtol=0)
+    torch.testing.assert_close(lse_seq, lse_til, atol=0, rtol=0)
+    do = torch.randn_like(o_til)
+    d_til = C.attn_bwd(do, qkv, o_til, lse_til, B, S, H, hd, hd ** -0.5, p, 99, kvl)
+    monkeypatch.setenv("MIFT_ATTN_SEQ", "2")
+    d_seq = C.attn_bwd(do, qkv, o_til, lse_til, B, S, H, hd, hd ** -0.5, p, 99, kvl)
+    torch.testing.assert_close(d_seq.float(), d_til.float(), atol=2e-3, rtol=2e-3)
+
+
 def test_flash_attention_kv_len():
     C = _C()
     torch.manual_seed(7)

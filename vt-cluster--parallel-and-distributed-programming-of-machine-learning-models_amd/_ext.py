@@ -36,10 +36,26 @@ def _load():
         spec = importlib.util.spec_from_file_location("mift._C", so)
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
+        if not os.environ.get("MIFT_EXT_SO") and os.environ.get("MIFT_ALLOW_STALE_EXT", "0") != "1":
+            _check_provenance(mod, so, here)
         sys.modules["mift._C"] = mod
         _C = mod
     except Exception as e:  # pragma: no cover - depends on build
         _ERR = e
+
+
+def _check_provenance(mod, so, here):
+    """The binary must have been built from the csrc/ tree next to it (build.py stamps the
+    sha256 of every source into the .so); a stale or foreign _C.so fails loudly."""
+    if not os.path.isdir(os.path.join(here, "csrc")):
+        return
+    import importlib
+    build = importlib.import_module(__package__ + ".build") if __package__ else None
+    want = build.source_digest(debug=os.path.basename(so).startswith("_C_debug")) if build else None
+    got = mod.source_hash() if hasattr(mod, "source_hash") else "<unstamped>"
+    if want is not None and got != want:
+        raise ImportError(f"stale extension {so}: built from sources {got[:12]}, tree is {want[:12]}; "
+                          f"rebuild with `python -m mift.build` (MIFT_ALLOW_STALE_EXT=1 to override)")
 
 
 def available() -> bool:

@@ -63,6 +63,8 @@ def build_argparser(defaults=None):
     ap.add_argument("--step_log", choices=["p1", "lab", "none"], default="p1")
     ap.add_argument("--no_save", action="store_true")
     ap.add_argument("--run_name", type=str, default=None, help="fixed run dir name (resume across jobs)")
+    ap.add_argument("--config", type=str, default=None,
+                    help="run config JSON (DeepSpeed keys + mift.* keys, mift.config.MiftConfig)")
     if defaults:
         ap.set_defaults(**defaults)
     return ap
@@ -83,7 +85,13 @@ def load_data(args, tok_vocab_pad, rank):
 def main(argv=None, defaults=None):
     args = build_argparser(defaults).parse_args(argv)
     torch.manual_seed(args.seed)
+    from ..config import MiftConfig
+    mcfg = MiftConfig.from_json(args.config)
+    mcfg.apply_env()
     ctx = D.init()
+    if ctx.rank == 0:
+        for line in mcfg.report():
+            print(line, flush=True)
     rank, world = ctx.rank, ctx.world
     gpu = ctx.device.type == "cuda"
     precision = args.precision or ("bf16" if gpu else "fp32")
@@ -135,8 +143,11 @@ def main(argv=None, defaults=None):
     batcher = MicroBatcher(ds, mb, acc, rank=ctx.dp_rank, world=ctx.dp, mode="strided")
     tcfg = TrainConfig(epochs=args.epochs, batch=mb, accum=acc, lr=args.lr, precision=precision,
                        logging_steps=args.logging_steps, save_steps=args.save_steps, max_steps=args.max_steps,
-                       output_dir=save_dir, resume=args.resume, recompute=bool(args.gradient_checkpointing),
-                       step_log=args.step_log, seed=args.seed)
+                       output_dir=save_dir, resume=args.resume,
+                       recompute=bool(args.gradient_checkpointing) or mcfg.activation_checkpointing,
+                       step_log=args.step_log, seed=args.seed, bucket_mb=mcfg.bucket_mb, graph=mcfg.graph,
+                       consistency_every=mcfg.consistency_every, max_grad_norm=mcfg.gradient_clipping,
+                       weight_decay=mcfg.weight_decay)
     trainer = Trainer(model, batcher, tcfg, ctx)
     logs.log("Trainer setup", time.perf_counter() - t0)
 

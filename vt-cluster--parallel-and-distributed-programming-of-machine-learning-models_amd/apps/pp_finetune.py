@@ -12,10 +12,12 @@ launch env (``RANK/WORLD_SIZE/LOCAL_RANK`` with SLURM fallbacks,
 ``zero_optimization.stage``, ``fp16/bf16.enabled``, ``optimizer.params``
 (betas, eps, weight_decay) and ``gradient_clipping`` are honoured; as in the
 reference, ``--accum`` and ``--lr`` from the CLI win (``engine.set_lr`` /
-``set_gradient_accumulation_steps``, `:207-208`).  Keys that only make sense
-for DeepSpeed-on-CPU (``cpu_offload``, ``partition_activations``,
-``cpu_checkpointing``) are accepted and ignored: 288 GB of HBM per GPU holds
-every stage's weights and in-flight activations.
+``set_gradient_accumulation_steps``, `:207-208`).  The JSON is parsed into the
+typed ``mift.config.MiftConfig`` (which also reads the ``mift.*`` MI355X keys):
+keys that only make sense for DeepSpeed-on-CPU (``cpu_offload``,
+``partition_activations``, ``cpu_checkpointing``) are accepted without effect and
+REPORTED at start-up (288 GB of HBM per GPU holds every stage's weights and
+in-flight activations); unknown keys are an error.
 
 Outputs: P2 loss lines ``[R{r}] ep=.. step=.. loss=.. (+..s)`` from the last
 stage every 10 steps (`:219-224`), ``{logdir}/timing_rank{r}.log`` phases, and
@@ -55,7 +57,8 @@ def build_argparser():
     ap.add_argument("--ds_cfg", default="deepspeed_pp_zero1_cpu.json")
     # mift extensions
     ap.add_argument("--pp", type=int, default=None, help="pipeline stages (default $PIPELINE_PARALLEL_SIZE or world)")
-    ap.add_argument("--partition", choices=["uniform", "balanced"], default="balanced")
+    ap.add_argument("--partition", choices=["uniform", "balanced"], default=None,
+                    help="layer split (default: mift.pp_partition / pipeline.partition_method, else balanced)")
     ap.add_argument("--precision", choices=["fp16", "bf16", "fp32"], default=None)
     ap.add_argument("--micro_batch", type=int, default=0,
                     help="GPU micro-batch: regroups batch*accum sequences per step into micro-batches of this "
@@ -79,23 +82,9 @@ def build_argparser():
 
 
 def read_ds_config(path):
-    """DeepSpeed JSON -> dict of the knobs we honour (missing file -> reference inline defaults)."""
-    d = {}
-    if path and os.path.isfile(path):
-        with open(path) as f:
-            d = json.load(f)
-    opt = d.get("optimizer", {}).get("params", {})
-    return {
-        "micro_batch": d.get("train_micro_batch_size_per_gpu"),
-        "zero_stage": int(d.get("zero_optimization", {}).get("stage", 1)),
-        "fp16": bool(d.get("fp16", {}).get("enabled", False)),
-        "bf16": bool(d.get("bf16", {}).get("enabled", False)),
-        "betas": tuple(opt.get("betas", (0.9, 0.999))),
-        "eps": float(opt.get("eps", 1e-8)),
-        "weight_decay": float(opt.get("weight_decay", 0.0)),
-        "clip": float(d.get("gradient_clipping", 1.0)),
-        "found": bool(d),
-    }
+    """DeepSpeed JSON (+ ``mift.*`` keys) -> mift.config.MiftConfig (missing file -> inline defaults)."""
+    from ..config import MiftConfig
+    return MiftConfig.from_json(path)
 
 
 def main(argv=None):
@@ -111,11 +100,15 @@ def main(argv=None):
 
     gpu = ctx.device.type == "cuda"
     ds = read_ds_config(args.ds_cfg)
-    precision = args.precision or ("fp32" if not gpu else ("bf16" if ds["bf16"] else "fp16"))
+    ds.apply_env()
+    if rank == 0:
+        for line in ds.report():
+            print(line, flush=True)
+    precision = args.precision or ("fp32" if not gpu else ("bf16" if ds.bf16 else "fp16"))
     if not gpu:
         precision = "fp32"
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[precision]
-    zero = args.zero if args.zero is not None else ds["zero_stage"]
+    zero = args.zero if args.zero is not None else ds.zero_stage
     logs = PhaseLogger(args.logdir, rank)
 
     # ---- data (every stage of a replica reads the same shard: DP rank, not global rank) ----
@@ -135,7 +128,7 @@ def main(argv=None):
     from ..models.opt import OPTConfig
     cfg = OPTConfig.preset(args.model_name)
     N = cfg.num_hidden_layers
-    split = partition_layers(N, ctx.pp, args.partition, head_cost_layers(cfg))
+    split = partition_layers(N, ctx.pp, args.partition or ds.pp_partition, head_cost_layers(cfg))
     lo, hi = stage_layer_range(split, ctx.pp_rank)
     model = build_causal_lm(args.model_name, dtype=dtype, device=ctx.device, seed=args.seed,
                             weights=args.base_weights, layer_range=(lo, hi), has_embed=ctx.is_first_stage,
@@ -164,16 +157,19 @@ def main(argv=None):
 
     # ---- engine ----
     t0 = time.perf_counter()
-    mb = ds["micro_batch"] or args.batch
+    mb = ds.micro_batch_size or args.batch
     per_step = mb * args.accum
-    if args.micro_batch and per_step % args.micro_batch == 0:
-        mb = args.micro_batch
+    gmb = args.micro_batch or ds.micro_batch
+    if gmb and per_step % gmb == 0:
+        mb = gmb
     accum = per_step // mb
     batcher = MicroBatcher(data, mb, accum, rank=ctx.dp_rank, world=ctx.dp)
     tcfg = TrainConfig(epochs=args.epochs, batch=mb, accum=accum, lr=args.lr, precision=precision,
-                       weight_decay=ds["weight_decay"], max_grad_norm=ds["clip"], logging_steps=args.log_every,
+                       weight_decay=ds.weight_decay, max_grad_norm=ds.gradient_clipping, logging_steps=args.log_every,
                        step_log="none", max_steps=args.max_steps, seed=args.seed, zero_stage=zero,
-                       recompute=bool(args.gradient_checkpointing), save_steps=args.save_steps,
+                       recompute=bool(args.gradient_checkpointing) or ds.activation_checkpointing,
+                       bucket_mb=ds.bucket_mb, graph=ds.graph, consistency_every=ds.consistency_every,
+                       save_steps=args.save_steps,
                        output_dir=os.path.join(args.out_root, "checkpoints") if args.save_steps else None,
                        resume=args.resume)
     t_last = [time.perf_counter()]

@@ -15,6 +15,24 @@
 
 #define MIFT_HD __device__ __forceinline__
 
+// Device-side bounds / shape checks: compiled only into the debug build (`python -m mift.build
+// --debug` -> _C_debug.so, -DMIFT_DEBUG=1); a failing check prints the site and traps, so the
+// faulting kernel is named by the fault itself (no GPU ASan on this pool).
+#if defined(MIFT_DEBUG) && MIFT_DEBUG
+#define MIFT_ASSERT(cond)                                                               \
+  do {                                                                                  \
+    if (!(cond)) {                                                                      \
+      printf("MIFT_ASSERT %s:%d: %s (block %d thread %d)\n", __FILE__, __LINE__, #cond, \
+             (int)blockIdx.x, (int)threadIdx.x);                                        \
+      __builtin_trap();                                                                 \
+    }                                                                                   \
+  } while (0)
+#else
+#define MIFT_ASSERT(cond) \
+  do {                    \
+  } while (0)
+#endif
+
 // Graph-replayable dropout seeds.  mift.models.layers.seed_for(base, step, site) =
 // fin(base*C1 + step*C2 + site*C3) with fin(x) = (x ^ x>>31) & (2^63-1).  Eager launches pass
 // the finished seed and sstep == nullptr.  Under hipGraph capture (mift.train.graph) the host

@@ -183,6 +183,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
   const T* Kg = Qg + D;
   const T* Vg = Qg + 2 * D;
   const int klen = kv_len ? kv_len[b] : S;
+  MIFT_ASSERT(klen >= 0 && klen <= S);
   const int q0 = qt * BQB + wave * 16 * QG;  // first query of this wave; group j: q0 + 16 j
   const float c2 = scale * LOG2E;
   const bool hz = (uint64_t)B * H * S * S < (1ull << 33);  // dropout pairs' high word is 0: hoisted hash
@@ -326,6 +327,185 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
   }
 }
 
+// ===================== forward, whole sequence in LDS ======================
+// Short sequences (distilgpt2 S = 256): one block of NW waves per (batch, head) stages ALL of K
+// (b128 image) and V (transpose-read image) in LDS once — one barrier per block instead of two
+// per 64-key tile, and K/V read from HBM once per head instead of once per query tile.  Each
+// wave takes 16-query groups in snake order (w, 2NW-1-w, 2NW+w, ...) so the causal work is
+// balanced across waves; the per-group math is the tiled kernel's, tile by tile from LDS.
+template <int HD>
+constexpr int seq_row_bytes() { return Geo<HD>::RS + Geo<HD>::TRS; }
+
+// MIFT_ATTN_SEQ: 0 = tiled kernels only, 1 = whole-sequence kernels when they fit and there are
+// >= 256 heads to fill the chip (default), 2 = whenever they fit (tests, A/B); read per call
+int attn_seq_mode() {
+  const char* e = getenv("MIFT_ATTN_SEQ");
+  return e ? atoi(e) : 1;
+}
+
+template <typename T, int HD, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_seq_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                              float* __restrict__ lse, const int* __restrict__ kv_len,
+                                                              int B, int S, int H, float scale, uint64_t seed,
+                                                              const int64_t* __restrict__ sstep, uint32_t thr,
+                                                              float inv_keep) {
+  seed = mift_seed(seed, sstep);
+  using G = Geo<HD>;
+  constexpr int NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int SP = (S + BKV - 1) / BKV * BKV;  // image rows (zero padded to whole key tiles)
+  char* Ks = smem;                           // [SP][RS] b128 image
+  char* Vs = smem + (size_t)SP * G::RS;      // [SP][TRS] tr image
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, qc = lane & 15;
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh % H;
+  const int D = H * HD;
+  const int64_t ld = 3LL * D;
+  const T* Qg = qkv + (int64_t)b * S * ld + h * HD;
+  const T* Kg = Qg + D;
+  const T* Vg = Qg + 2 * D;
+  const int klen = kv_len ? kv_len[b] : S;
+  MIFT_ASSERT(klen >= 0 && klen <= S);
+  const float c2 = scale * LOG2E;
+  const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
+  const uint32_t hm0 = mift_hmix(seed, 0);
+
+  // ---- stage K and V of the whole sequence: 8 chunks in flight per thread per round
+  {
+    constexpr int U = 4;
+    const int nch = SP * G::CH;
+    for (int c0 = tid; c0 < nch; c0 += U * NT) {
+      short8 kv[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = c0 + u * NT;
+        const int r = i / G::CH, c = i % G::CH;
+        if (i < nch && r < S) {
+          kv[u] = *reinterpret_cast<const short8*>(Kg + (int64_t)r * ld + c * 8);
+          vv[u] = *reinterpret_cast<const short8*>(Vg + (int64_t)r * ld + c * 8);
+        } else {
+          kv[u] = short8{0, 0, 0, 0, 0, 0, 0, 0};
+          vv[u] = short8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = c0 + u * NT;
+        if (i < nch) {
+          const int r = i / G::CH, c = i % G::CH;
+          *reinterpret_cast<short8*>(Ks + r * G::RS + c * 16) = kv[u];
+          *reinterpret_cast<short8*>(Vs + r * G::TRS + c * 16) = vv[u];
+        }
+      }
+    }
+    if (G::HDP != HD) {
+      constexpr int PADC = (G::HDP - HD) / 8;
+      for (int i = tid; i < SP * PADC; i += NT) {
+        const int r = i / PADC, c = HD / 8 + i % PADC;
+        *reinterpret_cast<short8*>(Ks + r * G::RS + c * 16) = short8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+  }
+  __syncthreads();
+
+  const int ng = (S + 15) / 16;
+  T* Og = out + (int64_t)b * S * D + h * HD;
+  for (int slot = 0;; ++slot) {
+    const int grp = (slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave;  // snake order
+    if (slot * NW >= ng) break;
+    if (grp >= ng) continue;
+    const int q0 = grp * 16, myq = q0 + qc;
+    vec8<T> qf[G::NKS];
+    load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
+    float m = -INFINITY, l = 0.f;
+    float4_ o[G::NOT];
+#pragma unroll
+    for (int i = 0; i < G::NOT; ++i) o[i] = float4_{0.f, 0.f, 0.f, 0.f};
+    const int kend = min(q0 + 16, klen);
+    const int nkt = (kend + BKV - 1) / BKV;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int k0 = kt * BKV;
+      float4_ st[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        st[t] = float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < G::NKS; ++s)
+          st[t] = mfma16(ld_frag<T>(Ks + (k0 + t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], st[t]);
+      }
+      const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = st[t][r] * c2;
+          if (diag) {
+            const int key = k0 + t * 16 + g * 4 + r;
+            if (key > myq || key >= klen) v = -INFINITY;
+          }
+          st[t][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const bool resc = __any(tmax > m + 8.f);
+      float alpha = 1.f;
+      if (resc) {
+        const float mnew = fmaxf(m, tmax);
+        alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mnew);
+        m = mnew;
+      }
+      vec8<T> pf[2];
+      float psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bool kp[4] = {true, true, true, true};
+        if (thr != 0) {
+          const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
+          if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
+          else mift_keep4(seed, i0, thr, kp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pv = (m == -INFINITY) ? 0.f : fast_exp2(st[t][r] - m);
+          psum += pv;
+          if (thr != 0) pv = kp[r] ? pv * inv_keep : 0.f;
+          pf[t >> 1][(t & 1) * 4 + r] = (T)pv;
+        }
+      }
+      l = l * alpha + psum;
+      if (resc) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ar = __shfl(alpha, g * 4 + r, 64);
+#pragma unroll
+          for (int i = 0; i < G::NOT; ++i) o[i][r] *= ar;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < G::NOT; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) o[i] = mfma16(pf[s2], tr_frag<T>(Vs, G::TRS, k0 + 32 * s2, i * 16, lane), o[i]);
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv_l = l > 0.f ? 1.f / l : 0.f;
+    if (g == 0 && myq < S) lse[(int64_t)bh * S + myq] = (l > 0.f) ? (m + log2f(l)) * LN2 : -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float il = __shfl(inv_l, g * 4 + r, 64);
+      const int q = q0 + g * 4 + r;
+      if (q < S) {
+#pragma unroll
+        for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (T)(o[i][r] * il);
+      }
+    }
+  }
+}
+
 // ============================ backward: dQ (+D) =============================
 template <typename T, int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
@@ -355,6 +535,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
   const T* dOg = dout + (int64_t)b * S * D + h * HD;
   const T* Og = o + (int64_t)b * S * D + h * HD;
   const int klen = kv_len ? kv_len[b] : S;
+  MIFT_ASSERT(klen >= 0 && klen <= S);
   const int q0 = qt * BQ + wave * 16;
   const int myq = q0 + qc;
   const float c2 = scale * LOG2E;
@@ -475,6 +656,7 @@ __global__ __launch_bounds__(256, HD <= 64 ? 3 : 1) void attn_bwd_dkdv_kernel(co
   const T* Vg = Qg + 2 * D;
   const T* dOg = dout + (int64_t)b * S * D + h * HD;
   const int klen = kv_len ? kv_len[b] : S;
+  MIFT_ASSERT(klen >= 0 && klen <= S);
   const int k0 = kt * BKV + wave * 16;
   const int mykey = k0 + kc;
   const float c2 = scale * LOG2E;
@@ -596,6 +778,281 @@ __global__ __launch_bounds__(256, HD <= 64 ? 3 : 1) void attn_bwd_dkdv_kernel(co
   }
 }
 
+// ================= backward, whole sequence in LDS (short S) =================
+// Same structure as attn_fwd_seq_kernel: one block of NW waves per (batch, head), the operand
+// rows of the whole sequence staged once in a single b128 image per tensor (the transposed
+// B-operand reads use ds_read_b64_tr_b16 on that same image: correct for any 8-B-aligned row
+// stride, a few bank conflicts instead of a second image), groups in snake order.
+template <typename T, int HD>
+MIFT_HD void stage_rows(char* img, const T* src, int64_t ld, int S, int SP, int tid, int nt) {
+  using G = Geo<HD>;
+  constexpr int U = 4;
+  const int nch = SP * G::CH;
+  for (int c0 = tid; c0 < nch; c0 += U * nt) {
+    short8 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = c0 + u * nt;
+      const int r = i / G::CH, c = i % G::CH;
+      v[u] = (i < nch && r < S) ? *reinterpret_cast<const short8*>(src + (int64_t)r * ld + c * 8)
+                                : short8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = c0 + u * nt;
+      if (i < nch) *reinterpret_cast<short8*>(img + (i / G::CH) * G::RS + (i % G::CH) * 16) = v[u];
+    }
+  }
+  if (G::HDP != HD) {
+    constexpr int PADC = (G::HDP - HD) / 8;
+    for (int i = tid; i < SP * PADC; i += nt)
+      *reinterpret_cast<short8*>(img + (i / PADC) * G::RS + (HD / 8 + i % PADC) * 16) = short8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+template <typename T, int HD, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
+                                                                 const T* __restrict__ dout, const float* __restrict__ lse,
+                                                                 float* __restrict__ Dv, T* __restrict__ dqkv,
+                                                                 const int* __restrict__ kv_len, int B, int S, int H,
+                                                                 float scale, uint64_t seed,
+                                                                 const int64_t* __restrict__ sstep, uint32_t thr,
+                                                                 float inv_keep) {
+  seed = mift_seed(seed, sstep);
+  using G = Geo<HD>;
+  constexpr int NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int SP = (S + BKV - 1) / BKV * BKV;
+  char* Ks = smem;                        // K rows (A of S^T; tr-read B of dQ)
+  char* Vs = smem + (size_t)SP * G::RS;   // V rows (A of dP^T)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, qc = lane & 15;
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh % H;
+  const int D = H * HD;
+  const int64_t ld = 3LL * D;
+  const T* Qg = qkv + (int64_t)b * S * ld + h * HD;
+  const T* Kg = Qg + D;
+  const T* Vg = Qg + 2 * D;
+  const T* dOg = dout + (int64_t)b * S * D + h * HD;
+  const T* Og = o + (int64_t)b * S * D + h * HD;
+  const int klen = kv_len ? kv_len[b] : S;
+  MIFT_ASSERT(klen >= 0 && klen <= S);
+  const float c2 = scale * LOG2E;
+  const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
+  const uint32_t hm0 = mift_hmix(seed, 0);
+  stage_rows<T, HD>(Ks, Kg, ld, S, SP, tid, NT);
+  stage_rows<T, HD>(Vs, Vg, ld, S, SP, tid, NT);
+  __syncthreads();
+  T* dQg = dqkv + (int64_t)b * S * ld + h * HD;
+  const int ng = (S + 15) / 16;
+  for (int slot = 0;; ++slot) {
+    const int grp = (slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave;
+    if (slot * NW >= ng) break;
+    if (grp >= ng) continue;
+    const int q0 = grp * 16, myq = q0 + qc;
+    vec8<T> qf[G::NKS], df[G::NKS];
+    load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
+    load_reg_frags<T, HD>(df, dOg, D, myq, S, lane);
+    float Dq = 0.f;
+    {
+      vec8<T> of[G::NKS];
+      load_reg_frags<T, HD>(of, Og, D, myq, S, lane);
+#pragma unroll
+      for (int s = 0; s < G::NKS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Dq += (float)of[s][e] * (float)df[s][e];
+      Dq += __shfl_xor(Dq, 16, 64);
+      Dq += __shfl_xor(Dq, 32, 64);
+      if (g == 0 && myq < S) Dv[(int64_t)bh * S + myq] = Dq;
+    }
+    const float lse2 = myq < S ? lse[(int64_t)bh * S + myq] * LOG2E : 0.f;
+    float4_ dq[G::NOT];
+#pragma unroll
+    for (int i = 0; i < G::NOT; ++i) dq[i] = float4_{0.f, 0.f, 0.f, 0.f};
+    const int kend = min(q0 + 16, klen);
+    const int nkt = (kend + BKV - 1) / BKV;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int k0 = kt * BKV;
+      vec8<T> dsf[2];
+      const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float4_ sa = float4_{0.f, 0.f, 0.f, 0.f}, pa = float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < G::NKS; ++s) {
+          sa = mfma16(ld_frag<T>(Ks + (k0 + t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], sa);
+          pa = mfma16(ld_frag<T>(Vs + (k0 + t * 16 + qc) * G::RS + (4 * s + g) * 16), df[s], pa);
+        }
+        bool kp[4] = {true, true, true, true};
+        if (thr != 0) {
+          const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
+          if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
+          else mift_keep4(seed, i0, thr, kp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pr = fast_exp2(sa[r] * c2 - lse2);
+          if (diag) {
+            const int key = k0 + t * 16 + g * 4 + r;
+            if (key > myq || key >= klen) pr = 0.f;
+          }
+          float dp = pa[r];
+          if (thr != 0) dp = kp[r] ? dp * inv_keep : 0.f;
+          dsf[t >> 1][(t & 1) * 4 + r] = (T)(pr * (dp - Dq));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < G::NOT; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) dq[i] = mfma16(dsf[s2], tr_frag<T>(Ks, G::RS, k0 + 32 * s2, i * 16, lane), dq[i]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + g * 4 + r;
+      if (q < S) {
+#pragma unroll
+        for (int i = 0; i < G::NOT; ++i) dQg[(int64_t)q * ld + i * 16 + qc] = (T)(dq[i][r] * scale);
+      }
+    }
+  }
+}
+
+template <typename T, int HD, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                                   const float* __restrict__ lse,
+                                                                   const float* __restrict__ Dv, T* __restrict__ dqkv,
+                                                                   const int* __restrict__ kv_len, int B, int S, int H,
+                                                                   float scale, uint64_t seed,
+                                                                   const int64_t* __restrict__ sstep, uint32_t thr,
+                                                                   float inv_keep) {
+  seed = mift_seed(seed, sstep);
+  using G = Geo<HD>;
+  constexpr int NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int SP = (S + BKV - 1) / BKV * BKV;
+  char* Qs = smem;                          // Q rows (A of S; tr-read B of dK)
+  char* dOs = smem + (size_t)SP * G::RS;    // dO rows (A of dP; tr-read B of dV)
+  float* lse_s = reinterpret_cast<float*>(dOs + (size_t)SP * G::RS);
+  float* D_s = lse_s + SP;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, kc = lane & 15;
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh % H;
+  const int D = H * HD;
+  const int64_t ld = 3LL * D;
+  const T* Qg = qkv + (int64_t)b * S * ld + h * HD;
+  const T* Kg = Qg + D;
+  const T* Vg = Qg + 2 * D;
+  const T* dOg = dout + (int64_t)b * S * D + h * HD;
+  const int klen = kv_len ? kv_len[b] : S;
+  MIFT_ASSERT(klen >= 0 && klen <= S);
+  const float c2 = scale * LOG2E;
+  stage_rows<T, HD>(Qs, Qg, ld, S, SP, tid, NT);
+  stage_rows<T, HD>(dOs, dOg, D, S, SP, tid, NT);
+  for (int i = tid; i < SP; i += NT) {
+    const int q = min(i, S - 1);
+    lse_s[i] = lse[(int64_t)bh * S + q] * LOG2E;
+    D_s[i] = Dv[(int64_t)bh * S + q];
+  }
+  __syncthreads();
+  T* dKg = dqkv + (int64_t)b * S * ld + D + h * HD;
+  T* dVg = dKg + D;
+  const int ng = (S + 15) / 16;
+  const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
+  const uint32_t hm0 = mift_hmix(seed, 0);
+  for (int slot = 0;; ++slot) {
+    const int grp = (slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave;
+    if (slot * NW >= ng) break;
+    if (grp >= ng) continue;
+    const int k0 = grp * 16, mykey = k0 + kc;
+    vec8<T> kf[G::NKS], vf[G::NKS];
+    load_reg_frags<T, HD>(kf, Kg, ld, mykey, S, lane);
+    load_reg_frags<T, HD>(vf, Vg, ld, mykey, S, lane);
+    float4_ dk[G::NOT], dv[G::NOT];
+#pragma unroll
+    for (int i = 0; i < G::NOT; ++i) {
+      dk[i] = float4_{0.f, 0.f, 0.f, 0.f};
+      dv[i] = float4_{0.f, 0.f, 0.f, 0.f};
+    }
+    // query tiles of 64 starting at the tile holding this group's first key (causal)
+    const int qt0 = k0 < klen ? k0 / BQ : SP / BQ;
+    for (int qb = qt0 * BQ; qb < S; qb += BQ) {
+      vec8<T> pf[2], dsf[2];
+      const bool interior = qb >= k0 + 15 && qb + BQ <= S && k0 + 16 <= klen;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float4_ sa = float4_{0.f, 0.f, 0.f, 0.f}, pa = float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < G::NKS; ++s) {
+          sa = mfma16(ld_frag<T>(Qs + (qb + t * 16 + kc) * G::RS + (4 * s + g) * 16), kf[s], sa);
+          pa = mfma16(ld_frag<T>(dOs + (qb + t * 16 + kc) * G::RS + (4 * s + g) * 16), vf[s], pa);
+        }
+        uint32_t hb[4] = {0, 0, 0, 0};
+        if (thr != 0) {
+          const int odd = kc & 1;
+          const int qa = min(qb + t * 16 + g * 4 + 2 * odd, S - 1);
+          const uint64_t p0 = (((uint64_t)bh * S + qa) * S + mykey) >> 1;
+          const uint64_t p1 = (((uint64_t)bh * S + min(qa + 1, S - 1)) * S + mykey) >> 1;
+          uint32_t h0, h1;
+          if (hz) {
+            h0 = mift_hash_lo(seed, hm0, (uint32_t)p0);
+            h1 = mift_hash_lo(seed, hm0, (uint32_t)p1);
+          } else {
+            h0 = mift_hash_pair(seed, p0);
+            h1 = mift_hash_pair(seed, p1);
+          }
+          const uint32_t o0 = __shfl_xor(h0, 1, 64), o1 = __shfl_xor(h1, 1, 64);
+          hb[0] = odd ? o0 : h0;
+          hb[1] = odd ? o1 : h1;
+          hb[2] = odd ? h0 : o0;
+          hb[3] = odd ? h1 : o1;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = qb + t * 16 + g * 4 + r;
+          bool valid = true;
+          float pr = fast_exp2(sa[r] * c2 - lse_s[ql]);
+          if (!interior) {
+            valid = ql < S && mykey <= ql && mykey < klen;
+            if (!valid) pr = 0.f;
+          }
+          float pd = pr, dp = pa[r];
+          if (thr != 0) {
+            const uint32_t bits = (S & 1) ? mift_bits16(seed, ((uint64_t)bh * S + ql) * S + mykey)
+                                          : ((hb[r] >> ((mykey & 1) << 4)) & 0xFFFFu);
+            const bool kp = valid && bits >= thr;
+            pd = kp ? pr * inv_keep : 0.f;
+            dp = kp ? dp * inv_keep : 0.f;
+          }
+          pf[t >> 1][(t & 1) * 4 + r] = (T)pd;
+          dsf[t >> 1][(t & 1) * 4 + r] = (T)(pr * (dp - D_s[ql]));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < G::NOT; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          dv[i] = mfma16(pf[s2], tr_frag<T>(dOs, G::RS, qb + 32 * s2, i * 16, lane), dv[i]);
+          dk[i] = mfma16(dsf[s2], tr_frag<T>(Qs, G::RS, qb + 32 * s2, i * 16, lane), dk[i]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = k0 + g * 4 + r;
+      if (key < S) {
+#pragma unroll
+        for (int i = 0; i < G::NOT; ++i) {
+          dKg[(int64_t)key * ld + i * 16 + kc] = (T)(dk[i][r] * scale);
+          dVg[(int64_t)key * ld + i * 16 + kc] = (T)dv[i][r];
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int HD>
 void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int* kvl, int B, int S, int H, float scale,
                 uint64_t seed, uint32_t thr, float inv_keep, hipStream_t st) {
@@ -604,7 +1061,23 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
   // 193 VGPRs (2 waves/SIMD vs 3) and measured slower on MI355X (tools/bench_attn.py: OPT-2.7B
   // fwd 75.2 vs 69.9 us, distilgpt2 41.0 vs 32.1 us, OPT-6.7B 243 vs 152 us): default 1
   static const int qg = [] { const char* e = getenv("MIFT_ATTN_QG"); return e ? atoi(e) : 1; }();
+  const int seq_env = attn_seq_mode();
   const int smem = G::ROW_BYTES + G::TR_BYTES;
+  // whole-sequence kernel when K and V of one head fit in LDS next to another block's (two
+  // blocks per CU) and there are enough heads to fill the chip with one block per head
+  const int SP = (S + BKV - 1) / BKV * BKV;
+  const int seq_smem = SP * seq_row_bytes<HD>();
+  if (seq_env && 2 * seq_smem <= 160 * 1024 && (B * H >= 256 || seq_env == 2)) {
+    auto kern = attn_fwd_seq_kernel<T, HD, 8>;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(B * H), dim3(512), seq_smem, st, (const T*)qkv.data_ptr(), (T*)o.data_ptr(),
+                       lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+    return;
+  }
   if (qg == 2) {
     const int nqt = (S + 2 * BQ - 1) / (2 * BQ);
     hipLaunchKernelGGL((attn_fwd_kernel<T, HD, 2>), dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
@@ -623,6 +1096,26 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
                 at::Tensor& Dv, at::Tensor& dqkv, const int* kvl, int B, int S, int H, float scale, uint64_t seed,
                 uint32_t thr, float inv_keep, hipStream_t st) {
   using G = Geo<HD>;
+  const int seq_env = attn_seq_mode();
+  const int SP = (S + BKV - 1) / BKV * BKV;
+  const int seq_dq = 2 * SP * G::RS, seq_kv = 2 * SP * G::RS + 2 * SP * 4;
+  if (seq_env && 2 * seq_kv <= 160 * 1024 && (B * H >= 256 || seq_env == 2)) {  // whole sequence in LDS, 2 blocks per CU
+    auto kq = attn_bwd_dq_seq_kernel<T, HD, 8>;
+    auto kk = attn_bwd_dkdv_seq_kernel<T, HD, 8>;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)kq, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)kk, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kq, dim3(B * H), dim3(512), seq_dq, st, (const T*)qkv.data_ptr(), (const T*)o.data_ptr(),
+                       (const T*)dout.data_ptr(), lse.data_ptr<float>(), Dv.data_ptr<float>(), (T*)dqkv.data_ptr(),
+                       kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+    hipLaunchKernelGGL(kk, dim3(B * H), dim3(512), seq_kv, st, (const T*)qkv.data_ptr(), (const T*)dout.data_ptr(),
+                       lse.data_ptr<float>(), Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed,
+                       mift_seed_step(), thr, inv_keep);
+    return;
+  }
   const int nqt = (S + BQ - 1) / BQ, nkt = (S + BKV - 1) / BKV;
   const int smem_dq = 2 * G::ROW_BYTES + G::TR_BYTES;
   hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD>), dim3(B * H * nqt), dim3(256), smem_dq, st, (const T*)qkv.data_ptr(),

@@ -83,11 +83,14 @@ template <typename T, typename W>
 __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ pos,
                                                     const W* __restrict__ wte, const W* __restrict__ wpe,
                                                     T* __restrict__ h, int S, int D, int pos_offset,
-                                                    uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
+                                                    uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep,
+                                                    int64_t vocab, int64_t npos) {
   seed = mift_seed(seed, sstep);
   const int row = blockIdx.x;
   const int64_t tok = ids[row];
   const int64_t p = (pos != nullptr ? pos[row] : (int64_t)(row % S)) + pos_offset;
+  MIFT_ASSERT(tok >= 0 && tok < vocab);
+  MIFT_ASSERT(wpe == nullptr || (p >= 0 && p < npos));
   for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
     float a[8], b[8];
     load8<W>(wte + tok * D + c, a);
@@ -179,7 +182,8 @@ at::Tensor mift_embed_fwd(const at::Tensor& ids, const c10::optional<at::Tensor>
   DISPATCH_16(out_dtype, embed_kernel<T, T><<<rows, 256, 0, st>>>(
                              ids.data_ptr<int64_t>(), pos ? pos->data_ptr<int64_t>() : nullptr, (const T*)wte.data_ptr(),
                              wpe ? (const T*)wpe->data_ptr() : nullptr, (T*)h.data_ptr(), S, D, (int)pos_offset,
-                             (uint64_t)seed, mift_seed_step(), thr_of(p), inv));
+                             (uint64_t)seed, mift_seed_step(), thr_of(p), inv, (int64_t)wte.size(0),
+                             wpe ? (int64_t)wpe->size(0) : (int64_t)0));
   return h;
 }
 
