@@ -215,22 +215,73 @@ def test_flash_attention_kv_len():
 
 @pytest.mark.parametrize("p", [0.0, 0.05])
 @pytest.mark.parametrize("K", [768, 3072])
-def test_lora_proj_and_wgrad(p, K):
+@pytest.mark.parametrize("M,nz", [(1000, 8), (1000, 24), (24576, 8)])
+def test_lora_proj_and_wgrad(p, K, M, nz):
+    """lora_proj for every block geometry (16- and 32-row blocks, one or two 16-column tiles:
+    non-zero rows 8 -> one tile, 24 -> two) incl. the tall OPT-size input that used to go to
+    torch.mm, and lora_wgrad, vs the fp32 reference."""
     C = _C()
     torch.manual_seed(8)
-    M = 1000
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.zeros(32, K, device="cuda", dtype=torch.bfloat16)
-    w[:8] = (torch.randn(8, K, device="cuda") * 0.05).to(torch.bfloat16)
-    out = C.lora_proj(x, w, 2.0, p, 55)
+    w[:nz] = (torch.randn(nz, K, device="cuda") * 0.05).to(torch.bfloat16)
+    out = C.lora_proj(x, w, 2.0, p, 55, nz)
     xd = ref.dropout(x.float(), p, 55)
     torch.testing.assert_close(out.float(), 2.0 * xd @ w.float().t(), atol=3e-2, rtol=3e-2)
+    if M > 4096:
+        return
     y = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
     acc = torch.zeros(K, 32, device="cuda")
     C.lora_wgrad(x, y, acc, p, 55, 0, 32, 0, 0)
     exp = xd.t() @ y.float()
     err = (acc - exp).norm() / exp.norm()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_lora_wgrad_group(dt):
+    """One grouped launch over a layer's worth of problems (kernels/lora.hip lora_wgrad_group):
+    dB in [P, r] layout from a column slice of a wider gradient, a dropout-masked dA in [r, P]
+    layout, a multi-slot dA (three adapters sharing one input, OPT q/k/v) and a ragged M —
+    each against the fp32 reference, accumulated into one flat arena."""
+    C = _C()
+    torch.manual_seed(21)
+    M, N, K = 1000, 3 * 256, 512
+    gz = torch.randn(M, N, device="cuda", dtype=dt)
+    x = torch.randn(M, K, device="cuda", dtype=dt)
+    T = torch.randn(M, 32, device="cuda", dtype=dt)
+    dT = torch.randn(M, 32, device="cuda", dtype=dt)
+    xr = torch.randn(333, 128, device="cuda", dtype=dt)
+    yr = torch.randn(333, 32, device="cuda", dtype=dt)
+    arena = torch.zeros(200000, device="cuda")
+    pad = [0, 0, 0] * 3
+    meta, xs, ys, ps, exp = [], [], [], [], []
+    # dB of the middle adapter: gz[:, 256:512], rank 8 at T columns 8..15 -> [256, 8] at offset 100
+    xs.append(gz[:, 256:512]); ys.append(T); ps.append(0.0)
+    meta += [1, 1, 8, 8, 100] + pad + [0]
+    exp.append((100, (gz[:, 256:512].float().t() @ T.float()[:, 8:16]).reshape(-1)))
+    # dA, dropout-masked input, rank 8 at columns 0..7 -> [8, K] at offset 5000
+    xs.append(x); ys.append(dT); ps.append(0.05)
+    meta += [2, 1, 0, 8, 5000] + pad + [77]
+    xd = ref.dropout(x.float(), 0.05, 77)
+    exp.append((5000, (xd.t() @ dT.float()[:, :8]).t().reshape(-1)))
+    # multi-slot dA: three rank-4 adapters in columns 0, 10, 20 of one product
+    xs.append(x); ys.append(dT); ps.append(0.0)
+    meta += [2, 3, 0, 4, 20000, 10, 4, 30000, 20, 4, 40000, 0, 0, 0, 0]
+    for q, off in [(0, 20000), (10, 30000), (20, 40000)]:
+        exp.append((off, (x.float().t() @ dT.float()[:, q:q + 4]).t().reshape(-1)))
+    # dense mode-0 problem with a ragged M
+    xs.append(xr); ys.append(yr); ps.append(0.0)
+    meta += [0, 1, 0, 32, 100000] + pad + [0]
+    exp.append((100000, (xr.float().t() @ yr.float()).reshape(-1)))
+    C.lora_wgrad_group(arena, xs, ys, meta, ps)
+    covered = torch.zeros_like(arena, dtype=torch.bool)
+    for off, e in exp:
+        got = arena[off:off + e.numel()]
+        err = (got - e).norm() / e.norm()
+        assert err < 1e-2, (off, err.item())
+        covered[off:off + e.numel()] = True
+    assert arena[~covered].abs().max().item() == 0.0  # nothing written outside the slots
 
 
 @pytest.mark.parametrize("rank,D", [(8, 768), (28, 2560), (16, 1024)])

@@ -72,6 +72,7 @@ struct LmArgs {
   int ntn;                // column tiles of the forward (= groups of the backward)
   int gpc;                // groups per split-K chunk
   float* partial;         // [S][M][N] fp32 split-K slabs
+  int dbg;                // MIFT_LM_DBG (diagnostics only): bit 0 = skip the E store
 };
 
 struct EpiArgs {
@@ -93,7 +94,25 @@ struct EpiArgs {
   float ext_inv_keep;
   const int64_t* sstep;    // device micro-step for graph-replayed dropout seeds (common.h mift_seed)
   int prefetch;            // epilogue: load aux / residual of all chunks up front (MIFT_EPI_PREFETCH=1; opt-in)
+  int group_m;             // tile raster: 0 = row panels (n fastest); g > 0 = groups of g row panels, m fastest
 };
+
+// Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
+// the tiles run in groups of g row panels with the row index fastest: the ~32 blocks an XCD holds at
+// once cover g row panels x 32/g column tiles, so each B (weight) tile is fetched once per group
+// instead of once per row panel.  The LM head (N = 50304, 197 column tiles) fetched its 77 MB
+// weight 32x from HBM in row-panel order (TCC_EA0_RDREQ 2.5x hipBLASLt's, tools/pmc_lmhead.sh).
+MIFT_HD void raster(int t, int ntm, int ntn, int g, int& tm, int& tn) {
+  if (g <= 1) {
+    tm = t / ntn;
+    tn = t % ntn;
+    return;
+  }
+  const int per = g * ntn, grp = t / per, first = grp * g;
+  const int gs = min(ntm - first, g), r = t - grp * per;
+  tm = first + r % gs;
+  tn = r / gs;
+}
 
 // Split-K tail (second launch of a hybrid data-parallel + split-K GEMM): the
 // ragged last wave of tiles [tile0, tile0 + ntiles) is cut into gx k-chunks per
@@ -512,6 +531,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   #pragma unroll
         for (int e = 0; e < 8; ++e) z[e] += rv[e];
       }
+      if (ep.lm.dbg & 1) return;  // diagnostics: MIFT_LM_DBG bit 0 skips the C store
       if (full) store8<T>(C + off, z);
       else for (int e = 0; e < N - gc; ++e) C[off + e] = (T)z[e];
     };
@@ -530,15 +550,26 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     }
   };
 
-  // ---- EPI 1: LM-head forward epilogue (see LmArgs) — registers only, the ring is reused for
-  // two [NW][WM] row-partial arrays (max, sum) exchanged between the NWN waves of a row.
+  // ---- EPI 1: LM-head forward epilogue (see LmArgs).  The 16-bit E tile is staged in LDS
+  // (the ring is reused) and written out as whole-row 16-B chunks: storing it straight from the
+  // accumulator layout (32-B row pieces per lane group) cost ~140 us of the 820 us distilgpt2 head
+  // (tools/diag_lmhead.py), the coalesced copy-out hides under the next tiles' main loops like the
+  // plain GEMM's.  Two [NW][WM] row-partial arrays (max, sum) behind the C tile exchange the NWN
+  // waves' partials of a row.
   auto lm_fwd_epilogue = [&]() {
     const LmArgs& lm = ep.lm;
+    constexpr int CLD = BN + 8;
     __syncthreads();  // every wave is done reading the staging ring
-    float* redm = reinterpret_cast<float*>(smem);
+    T* Cs = reinterpret_cast<T*>(smem);
+    float* redm = reinterpret_cast<float*>(smem + BM * CLD * sizeof(T));
     float* reds = redm + NW * WM;
     const int V = lm.V;
     constexpr float L2E = 1.4426950408889634f;
+    // labels first: their load latency hides under the max pass (they are consumed after a barrier)
+    int64_t labs[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) labs[i] = lm.labels[min(m0 + wm * WM + i * 16 + fr, M - 1)];
+    const bool full = n0 + BN <= V;  // block-uniform: only the last column tile holds padding columns
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       float m = -INFINITY;
@@ -546,7 +577,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + wn * WN + j * 16 + fq * 4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m = (col + e < V) ? fmaxf(m, acc[i][j][e]) : m;
+        for (int e = 0; e < 4; ++e) m = (full || col + e < V) ? fmaxf(m, acc[i][j][e]) : m;
       }
       m = fmaxf(m, __shfl_xor(m, 16, 64));
       m = fmaxf(m, __shfl_xor(m, 32, 64));
@@ -559,18 +590,20 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
 #pragma unroll
       for (int w = 0; w < NWN; ++w) m = fmaxf(m, redm[(wm * NWN + w) * WM + i * 16 + fr]);
       if (m == -INFINITY) m = 0.f;  // tile entirely beyond V (cannot happen for V_pad - V < BN)
-      const int row = m0 + wm * WM + i * 16 + fr;
-      const bool rok = row < M;
-      const int64_t lab = rok ? lm.labels[row] : -1;
+      const int lrow = wm * WM + i * 16 + fr;
+      const int row = m0 + lrow;
+      const int64_t lab = row < M ? labs[i] : -1;
       const float mb = m * L2E;
       float s = 0.f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * WN + j * 16 + fq * 4;
+        const int lcol = wn * WN + j * 16 + fq * 4;
+        const int col = n0 + lcol;
         float ev[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          ev[e] = (col + e < V) ? __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][e], L2E, -mb)) : 0.f;
+          ev[e] = (lm.dbg & 2) ? acc[i][j][e]
+                  : (full || col + e < V) ? __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][e], L2E, -mb)) : 0.f;
           s += ev[e];
         }
         const int64_t d = lab - col;
@@ -578,7 +611,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
           const float4_ a = acc[i][j];
           lm.zlab[row] = d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
         }
-        if (rok && col < N) store4<T>(C + (size_t)row * ldc + col, ev);
+        store4<T>(Cs + lrow * CLD + lcol, ev);
       }
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
@@ -597,26 +630,47 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       if (m == -INFINITY) m = 0.f;
       if (row < M) lm.stats[(size_t)row * lm.ntn + n0 / BN] = make_float2(m, s);
     }
+    if (lm.dbg & 1) return;
+    constexpr int VPR = BN / 8;
+    static_assert((BM * VPR) % NT == 0, "E copy-out chunks must split evenly over the threads");
+#pragma unroll 4
+    for (int it = 0; it < BM * VPR / NT; ++it) {
+      const int v = tid + it * NT;
+      const int r = v / VPR, c8 = (v % VPR) * 8;
+      const int gr = m0 + r, gc = n0 + c8;
+      if (gr < M && gc < N)
+        *reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc) = *reinterpret_cast<const short8*>(Cs + r * CLD + c8);
+    }
   };
 
   const int nk_all = K / BK;
   if constexpr (EPI == 1) {
     static_assert(NSTAGE == 0, "LM-head forward runs on the phased 256x256 tile");
-    const int nblk = gridDim.x;
-    int bid = blockIdx.x;
-    {
-      const int q = nblk / 8, r = nblk % 8;
-      const int xcd = bid % 8, loc = bid / 8;
-      bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    // persistent when gridDim.x < tiles (MIFT_LM_PERSIST): block b walks tiles b, b + grid, ...,
+    // all on its own XCD (grid % 8 == 0), so the E stores of one tile drain while the next tile's
+    // main loop runs instead of holding the CU until the block retires
+    const int nblk = ntm * ntn;
+    for (int t0 = blockIdx.x; t0 < nblk; t0 += gridDim.x) {
+      int bid = t0;
+      {
+        const int q = nblk / 8, r = nblk % 8;
+        const int xcd = bid % 8, loc = bid / 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+      }
+      {
+        int tm, tn;
+        raster(bid, ntm, ntn, ep.group_m, tm, tn);
+        m0 = tm * BM;
+        n0 = tn * BN;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+      mainloop8(0, nk_all, [](int) {});
+      lm_fwd_epilogue();
+      __syncthreads();  // the E tile in LDS is read out before the next prologue restages the ring
     }
-    m0 = (bid / ntn) * BM;
-    n0 = (bid % ntn) * BN;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
-    mainloop8(0, nk_all, [](int) {});
-    lm_fwd_epilogue();
     return;
   } else if constexpr (EPI == 2) {
     // ---- LM-head dgrad on the phased 256x256 tile.  A = E [M, V_pad], B = Wᵀ [N, V_pad].
@@ -690,8 +744,12 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       const int xcd = bid % 8, loc = bid / 8;
       bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
     }
-    m0 = (bid / ntn) * BM;
-    n0 = (bid % ntn) * BN;
+    {
+      int tm, tn;
+      raster(bid, ntm, ntn, ep.group_m, tm, tn);
+      m0 = tm * BM;
+      n0 = tn * BN;
+    }
     if constexpr (NSTAGE == 0) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -711,8 +769,12 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     const int S = sk.gx;
     const int tl = blockIdx.x / S, cidx = blockIdx.x % S;
     const int tile = sk.tile0 + tl;
-    m0 = (tile / ntn) * BM;
-    n0 = (tile % ntn) * BN;
+    {
+      int tm, tn;
+      raster(tile, ntm, ntn, ep.group_m, tm, tn);  // same raster as the data-parallel launch
+      m0 = tm * BM;
+      n0 = tn * BN;
+    }
     mainloop((int)((long)cidx * nk_all / S), (int)((long)(cidx + 1) * nk_all / S));
     constexpr int SLOT = TM * TN * NT;  // float4 per partial tile
     if (cidx < S - 1) {
@@ -770,6 +832,12 @@ int* sk_flags(int n) {
 int sk_mode_env() {
   static int v = [] { const char* e = getenv("MIFT_GEMM_SK"); return e ? atoi(e) : -1; }();
   return v;  // -1 auto, 0 off, 1 force
+}
+
+// tile raster group (EpiArgs::group_m): MIFT_GEMM_GROUP (read per call, A/B-able) or the default
+int gemm_group_m(int N) {
+  if (const char* e = getenv("MIFT_GEMM_GROUP")) return atoi(e);
+  return N >= 8192 ? 4 : 0;
 }
 
 template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE>
@@ -958,8 +1026,15 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   ep.lm.stats = reinterpret_cast<float2*>(stats.data_ptr<float>());
   ep.lm.zlab = zlab.data_ptr<float>();
   ep.lm.ntn = ntn;
+  if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);
+  {
+    const char* g = getenv("MIFT_GEMM_GROUP");  // row-panel order measured best for the fused head
+    ep.group_m = g ? atoi(g) : 0;
+  }
   SkArgs sk{};
-  constexpr int SMEM = 2 * (BM + BN) * ROWB;
+  // staging ring (128 KiB) reused for the E tile + the two row-partial arrays
+  constexpr int SMEM = std::max(2 * (BM + BN) * ROWB, BM * (BN + 8) * 2 + 2 * 8 * (BM / 2) * 4);
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
   auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>;
   static bool attr = false;
   if (!attr) {
@@ -967,7 +1042,15 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
     attr = true;
   }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-  hipLaunchKernelGGL(kern, dim3(ntm * ntn), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
+  int grid = ntm * ntn;
+  {
+    // blocks per CU of the persistent grid (0 = one block per tile): one per CU measured 3-6 % faster
+    // than one block per tile (tools/diag_lmhead.py: 772 vs 793 us, 788 vs 836 us on two boxes)
+    const char* pe = getenv("MIFT_LM_PERSIST");
+    const int per = pe ? atoi(pe) : 1;
+    if (per > 0) grid = std::min(grid, per * num_cus());
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
                      (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
   hipLaunchKernelGGL(lmhead_lse_kernel, dim3((M + 3) / 4), dim3(256), 0, st,
                      reinterpret_cast<const float2*>(stats.data_ptr<float>()), ntn, zlab.data_ptr<float>(),
@@ -1029,7 +1112,7 @@ std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w
   TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1), "lmhead_fwd: a [M,K], w [V_pad,K]");
   TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && a.size(1) % 64 == 0, "lmhead_fwd: K-contiguous, K % 64 == 0");
   TORCH_CHECK(a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "lmhead_fwd: 16-B aligned rows");
-  TORCH_CHECK(w.size(0) % 4 == 0 && V <= w.size(0) && w.size(0) - V < 256, "lmhead_fwd: V_pad % 4, V_pad - V < 256");
+  TORCH_CHECK(w.size(0) % 8 == 0 && V <= w.size(0) && w.size(0) - V < 256, "lmhead_fwd: V_pad % 8, V_pad - V < 256");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == a.size(0),
               "lmhead_fwd: int64 labels [M]");
   TORCH_CHECK(a.scalar_type() == w.scalar_type(), "lmhead_fwd: dtype mismatch");
@@ -1129,6 +1212,8 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     const char* e = getenv("MIFT_EPI_PREFETCH");  // read per call: A/B-able within one process
     ep.prefetch = e ? atoi(e) : 0;
   }
+  ep.group_m = gemm_group_m(N);
+  if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);  // diagnostics (bit 0: no C store)
   ep.pre_add = nullptr;
   if (pre_add) {
     TORCH_CHECK(pre_add->size(0) == M && pre_add->size(1) == N && pre_add->stride(0) == c.stride(0) &&

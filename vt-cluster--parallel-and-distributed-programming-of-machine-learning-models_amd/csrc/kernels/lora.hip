@@ -21,6 +21,8 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include <tuple>
+
 namespace {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -58,57 +60,59 @@ MIFT_HD frag_t<T> masked_frag(const T* p, uint64_t seed, uint64_t idx0, uint32_t
 }
 
 // ------------------------------------------------------------------ lora_proj
-// Grid = (M/32 row blocks) x KS K-splits: with only M/32 row blocks (128 for
-// M = 4096) the kernel filled half of the 256 CUs and ran latency-bound; the
-// K-splits give ~1024 blocks.  KS > 1: every block stores its [32,32] fp32
-// partial to ws[kss] with plain stores and lora_proj_reduce sums the KS
-// partials into the 16-bit output (an in-kernel last-block reduction needs a
-// device-scope fence per block, ~3.5 us on gfx950 — slower than a launch).
-template <typename T, int NW>
+// Grid = (M/(16·MT) row blocks) x KS K-splits.  MT = 1 (16 rows per block) doubles the blocks of a
+// distilgpt2-size M (8192 rows -> 512 blocks, two per CU) so more X bytes are in flight per CU;
+// NTI = 1 when only the first 16 rows of W are non-zero (one adapter, r <= 16): half the MFMAs
+// and W loads of the 32-column product.  KS > 1: every block stores its fp32 partial to ws[kss]
+// with plain stores and lora_proj_reduce sums the KS partials into the 16-bit output (an
+// in-kernel last-block reduction needs a device-scope fence per block, ~3.5 us on gfx950).
+template <typename T, int NW, int MT, int NTI>
 __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict__ X, const T* __restrict__ W,
                                                         T* __restrict__ out, int M, int K, int ldx, float alpha,
                                                         uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep, int KS,
                                                         float* __restrict__ ws) {
   seed = mift_seed(seed, sstep);
-  __shared__ float red[NW][32][33];
+  constexpr int RB = 16 * MT;  // rows per block
+  __shared__ float red[NW][RB][33];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, fr = lane & 15;
   const int mb = blockIdx.x / KS, kss = blockIdx.x % KS;
-  const int m0 = mb * 32;
-  float4_ acc[2][2];
+  const int m0 = mb * RB;
+  float4_ acc[MT][NTI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
-  const int rows[2] = {min(m0 + fr, M - 1), min(m0 + 16 + fr, M - 1)};
+    for (int j = 0; j < NTI; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+  int rows[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) rows[i] = min(m0 + 16 * i + fr, M - 1);
   const int nks_all = K / 32;
   const int per_blk = (nks_all + KS - 1) / KS;
   const int kb0 = kss * per_blk, nks = min(nks_all, kb0 + per_blk);
-  // each wave owns a contiguous K range of the block's split; UNR k-steps of
-  // loads are issued back to back before their MFMAs (memory-level
-  // parallelism: one 16-B load per lane per operand per k-step).  NW = 8 for
-  // long K halves every wave's chain of dependent load rounds.
-  constexpr int UNR = 4;
+  // each wave owns a contiguous K range of the block's split; UNR k-steps of loads are issued
+  // back to back before their MFMAs (memory-level parallelism: one 16-B X load per lane per
+  // M-tile per k-step)
+  constexpr int UNR = MT == 1 ? 8 : 4;
   const int per = (nks - kb0 + NW - 1) / NW;
   const int kbeg = kb0 + wave * per, kend = min(nks, kbeg + per);
   for (int ks0 = kbeg; ks0 < kend; ks0 += UNR) {
-    short8 ra[UNR][2], rb[UNR][2];
+    short8 ra[UNR][MT], rb[UNR][NTI];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int col = min(ks0 + u, nks - 1) * 32 + g * 8;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) ra[u][i] = *reinterpret_cast<const short8*>(X + (int64_t)rows[i] * ldx + col);
+      for (int i = 0; i < MT; ++i) ra[u][i] = *reinterpret_cast<const short8*>(X + (int64_t)rows[i] * ldx + col);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) rb[u][j] = *reinterpret_cast<const short8*>(W + (int64_t)(j * 16 + fr) * K + col);
+      for (int j = 0; j < NTI; ++j) rb[u][j] = *reinterpret_cast<const short8*>(W + (int64_t)(j * 16 + fr) * K + col);
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       if (ks0 + u >= kend) break;
       const int col = (ks0 + u) * 32 + g * 8;
-      frag_t<T> a[2], b[2];
+      frag_t<T> a[MT], b[NTI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < MT; ++i) {
         short8 v = ra[u][i];
         if (thr != 0) {
           bool kp[8];
@@ -126,19 +130,19 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict_
         __builtin_memcpy(&a[i], &v, 16);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) __builtin_memcpy(&b[j], &rb[u][j], 16);
+      for (int j = 0; j < NTI; ++j) __builtin_memcpy(&b[j], &rb[u][j], 16);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<T>(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < NTI; ++j) acc[i][j] = mfma16<T>(a[i], b[j], acc[i][j]);
     }
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[wave][i * 16 + g * 4 + r][j * 16 + fr] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) red[wave][i * 16 + g * 4 + r][j * 16 + fr] = j < NTI ? acc[i][j < NTI ? j : 0][r] : 0.f;
   __syncthreads();
   auto rsum = [&](int r, int c) {
     float v = 0.f;
@@ -147,14 +151,14 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict_
     return v;
   };
   if (KS == 1) {
-    for (int e = tid; e < 32 * 32; e += NW * 64) {
+    for (int e = tid; e < RB * 32; e += NW * 64) {
       const int r = e >> 5, c = e & 31;
       if (m0 + r < M) out[(int64_t)(m0 + r) * 32 + c] = (T)(rsum(r, c) * alpha);
     }
     return;
   }
   float* wp = ws + (int64_t)kss * M * 32;
-  for (int e = tid; e < 32 * 32; e += NW * 64) {
+  for (int e = tid; e < RB * 32; e += NW * 64) {
     const int r = e >> 5, c = e & 31;
     if (m0 + r < M) wp[(int64_t)(m0 + r) * 32 + c] = rsum(r, c);
   }
@@ -188,12 +192,46 @@ MIFT_HD v4s tr_read(const char* lds_base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(lds_base + off));
 }
 
+// Grouped: ONE launch reduces every weight-gradient problem of a layer's backward (dB and dA of
+// each adapter, up to WG_MAXP).  Block b belongs to the problem whose [blk0, next blk0) holds it;
+// a problem is split into P/64 column tiles x ceil(M / rows) row chunks.  One launch per layer
+// instead of two per adapter: the per-adapter launches were ~10 us each for 12-50 MB of reads
+// (ramp + tail dominate), 0.43 ms of the 5.8 ms distilgpt2 step on the critical path even on the
+// side stream (tools/step_ab.py, MIFT_DIAG_SKIP=wgrad).
+constexpr int WG_MAXP = 16, WG_MAXS = 4;
+struct WgSlot {
+  int qoff, rank;   // columns [qoff, qoff + rank) of the 32-wide product ...
+  int64_t offset;   // ... land at out + offset in dB [P, rank] (mode 1) / dA [rank, P] (mode 2) layout
+};
+struct WgProb {
+  const void* X;    // [M, P] rows of stride ldx (a column slice of a wider tensor is fine)
+  const void* Y;    // [M, 32] contiguous
+  int ldx, P, M, rows, blk0, mode, nslot;
+  uint32_t thr;     // LoRA-input dropout on X (dA): keep iff hash >= thr, index = row * P + col
+  float inv_keep;
+  uint64_t seed;
+  WgSlot slot[WG_MAXS];
+};
+struct WgArgs {
+  float* out;
+  const int64_t* sstep;
+  int np;
+  WgProb p[WG_MAXP];
+};
+
 template <typename T>
-__global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X, const T* __restrict__ Y,
-                                                         float* __restrict__ out, int M, int P, int ldx,
-                                                         int rows_per_block, uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr,
-                                                         float inv_keep, int mode, int rank, int qoff) {
-  seed = mift_seed(seed, sstep);
+__global__ __launch_bounds__(256) void lora_wgrad_kernel(const WgArgs args) {
+  int pi = 0;
+#pragma unroll 1
+  while (pi + 1 < args.np && (int)blockIdx.x >= args.p[pi + 1].blk0) ++pi;
+  const WgProb& pr = args.p[pi];
+  const T* __restrict__ X = reinterpret_cast<const T*>(pr.X);
+  const T* __restrict__ Y = reinterpret_cast<const T*>(pr.Y);
+  const int M = pr.M, P = pr.P, ldx = pr.ldx, rows_per_block = pr.rows;
+  const uint32_t thr = pr.thr;
+  const float inv_keep = pr.inv_keep;
+  const uint64_t seed = mift_seed(pr.seed, args.sstep);
+  const int lb = blockIdx.x - pr.blk0;
   // NB 32-row steps per group: the whole group's global loads are in flight
   // together (one 16-B X load + half a Y load per thread per step), staged
   // into NB LDS buffers, then consumed; the next group's loads are issued
@@ -205,10 +243,11 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, li = lane & 15;
   const int ntp = P / 64;
-  const int pt = blockIdx.x % ntp, ms = blockIdx.x / ntp;
+  const int pt = lb % ntp, ms = lb / ntp;
   const int p0 = pt * 64;
   const int mbeg = ms * rows_per_block;
   const int mend = min(mbeg + rows_per_block, M);
+  MIFT_ASSERT(P % 64 == 0 && mbeg < M);
   float4_ acc[2] = {float4_{0.f, 0.f, 0.f, 0.f}, float4_{0.f, 0.f, 0.f, 0.f}};
 
   const int xr = tid >> 3, xc = tid & 7;
@@ -291,24 +330,36 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const T* __restrict__ X
     }
   }
   // acc[c][r] = out[p = p0 + wave*16 + g*4 + r][q = c*16 + li]
-  // mode 0: dense [P,32]; mode 1: dB layout [P, rank]; mode 2: dA layout [rank, P]
+  // mode 0: dense [P,32] at out + slot[0].offset; mode 1: dB [P, rank]; mode 2: dA [rank, P] per slot
+  float* out = args.out;
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t pp = p0 + wave * 16 + g * 4 + r;
       const int q = c * 16 + li;
-      if (mode == 0) atomicAdd(out + pp * 32 + q, acc[c][r]);
-      else if (q >= qoff && q < qoff + rank) atomicAdd(out + (mode == 1 ? pp * rank + (q - qoff) : (int64_t)(q - qoff) * P + pp), acc[c][r]);
+      if (pr.mode == 0) {
+        atomicAdd(out + pr.slot[0].offset + pp * 32 + q, acc[c][r]);
+        continue;
+      }
+#pragma unroll 1
+      for (int si = 0; si < pr.nslot; ++si) {
+        const WgSlot& sl = pr.slot[si];
+        if (q >= sl.qoff && q < sl.qoff + sl.rank)
+          atomicAdd(out + sl.offset + (pr.mode == 1 ? pp * sl.rank + (q - sl.qoff) : (int64_t)(q - sl.qoff) * P + pp),
+                    acc[c][r]);
+      }
     }
 }
 
 }  // namespace
 
-at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed) {
+at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed,
+                          int64_t rows) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "lora_proj: x [M,K] row-major");
   TORCH_CHECK(w.is_contiguous() && w.size(0) == 32 && w.size(1) == x.size(1), "lora_proj: w [32,K]");
   TORCH_CHECK(x.scalar_type() == w.scalar_type(), "lora_proj: dtype");
+  TORCH_CHECK(rows >= 1 && rows <= 32, "lora_proj: non-zero rows of w in [1, 32]");
   const int M = x.size(0), K = x.size(1);
   TORCH_CHECK(K % 32 == 0 && x.stride(0) % 8 == 0, "lora_proj: K % 32, aligned rows");
   auto out = at::empty({M, 32}, x.options());
@@ -316,12 +367,19 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const uint32_t thr = mift_thr16(p);
   const float ik = p > 0 ? mift_inv_keep(p) : 1.f;
-  const int mblocks = (M + 31) / 32, nks = K / 32;
-  // K-splits so the launch covers the chip (>= ~1024 blocks), >= 4 k-steps (one per wave) each
+  const int cus = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  // 16-row blocks while 32-row blocks would leave fewer than two per CU (MIFT_LORA_MT=1|2 forces)
+  const char* mte = getenv("MIFT_LORA_MT");
+  const int MT = mte ? (atoi(mte) == 1 ? 1 : 2) : ((M + 31) / 32 >= 2 * cus ? 2 : 1);
+  const int mblocks = (M + 16 * MT - 1) / (16 * MT), nks = K / 32;
   static const int ks_env = [] { const char* e = getenv("MIFT_LORA_KS"); return e ? atoi(e) : 0; }();
-  // split K only when the row blocks alone leave CUs idle (measured: distilgpt2, M = 8192 ->
-  // 256 row blocks, is 3 % faster unsplit; OPT micro-batches of M = 4096 gain 2 % from KS = 8)
-  int KS = mblocks >= 192 ? 1 : std::max(1, std::min(std::max(1, nks / 4), (1024 + mblocks - 1) / mblocks));
+  // K-splits only when the row blocks alone leave CUs idle (>= ~1024 blocks, >= 4 k-steps each)
+  int KS = mblocks >= 2 * cus ? 1 : std::max(1, std::min(std::max(1, nks / 4), (1024 + mblocks - 1) / mblocks));
   if (ks_env > 0) KS = std::max(1, std::min(ks_env, std::max(1, nks / 4)));  // A/B override
   float* ws = nullptr;
   at::Tensor wsb;
@@ -330,21 +388,18 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
     ws = wsb.data_ptr<float>();
   }
   const int grid = mblocks * KS;
-  // 4 waves per row block (MIFT_LORA_NW=8 for 8): the 8-wave variant for long K measured slower
-  // at OPT-2.7B shapes (M = 24576: K = 2560 35.6 vs 30.3 us, K = 7680 118 vs 105, K = 10240 155 vs
-  // 140; tools/bench_rowproj.py) and even at distilgpt2's
-  static const int nw_env = [] { const char* e = getenv("MIFT_LORA_NW"); return e ? atoi(e) : 4; }();
-  const bool wide = nw_env == 8;
+  const bool one_tile = rows <= 16;
   auto go = [&](auto tt) {
     using T = decltype(tt);
-    if (wide)
-      lora_proj_kernel<T, 8><<<grid, 512, 0, st>>>((const T*)x.data_ptr(), (const T*)w.data_ptr(),
-                                                   (T*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                   (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
-    else
-      lora_proj_kernel<T, 4><<<grid, 256, 0, st>>>((const T*)x.data_ptr(), (const T*)w.data_ptr(),
-                                                   (T*)out.data_ptr(), M, K, (int)x.stride(0), (float)alpha,
-                                                   (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
+    auto args = std::make_tuple((const T*)x.data_ptr(), (const T*)w.data_ptr(), (T*)out.data_ptr(), M, K,
+                                (int)x.stride(0), (float)alpha, (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
+    auto launch = [&](auto kern) {
+      std::apply([&](auto... a) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a...); }, args);
+    };
+    if (MT == 1 && one_tile) launch(lora_proj_kernel<T, 4, 1, 1>);
+    else if (MT == 1) launch(lora_proj_kernel<T, 4, 1, 2>);
+    else if (one_tile) launch(lora_proj_kernel<T, 4, 2, 1>);
+    else launch(lora_proj_kernel<T, 4, 2, 2>);
   };
   if (x.scalar_type() == at::kBFloat16) go(bf16{});
   else go(fp16{});
@@ -358,35 +413,98 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   return out;
 }
 
-// out fp32, accumulated: mode 0 -> out[P,32]; mode 1/2 -> out is a flat arena
-// and the result lands at out[offset:] in dB [P,r] / dA [r,P] layout.
+namespace {
+template <typename T>
+void launch_wgrad(WgArgs& args, hipStream_t st) {
+  // rows per block: ~2048 blocks over the group (eight per CU: loads of several blocks in flight
+  // per CU), a multiple of the 128-row load group, >= 128 (MIFT_WGRAD_BLOCKS: A/B knob)
+  const char* te = getenv("MIFT_WGRAD_BLOCKS");
+  const int64_t target = te ? std::max(1, atoi(te)) : 2048;
+  int64_t work = 0;
+  for (int i = 0; i < args.np; ++i) work += (int64_t)(args.p[i].P / 64) * args.p[i].M;
+  const int64_t rows = std::max<int64_t>(128, (work / target + 127) / 128 * 128);
+  int blk = 0;
+  for (int i = 0; i < args.np; ++i) {
+    WgProb& p = args.p[i];
+    p.rows = (int)std::min<int64_t>(rows, (p.M + 127) / 128 * 128);
+    p.blk0 = blk;
+    blk += (p.P / 64) * ((p.M + p.rows - 1) / p.rows);
+  }
+  if (blk > 0) lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
+}
+}  // namespace
+
+// Grouped LoRA weight gradients into a flat fp32 tensor `out` (the grad arena, or a dense [P,32]):
+//   xs[i] [M_i, P_i] (row stride free, unit column stride), ys[i] [M_i, 32];
+//   meta[i] = {mode, nslot, (qoff, rank, offset) x WG_MAXS, seed};  ps[i] = LoRA-input dropout p on xs[i].
+void mift_lora_wgrad_group(at::Tensor& out, const std::vector<at::Tensor>& xs, const std::vector<at::Tensor>& ys,
+                           const std::vector<int64_t>& meta, const std::vector<double>& ps) {
+  const int np = (int)xs.size();
+  constexpr int MW = 3 + 3 * WG_MAXS;
+  TORCH_CHECK(np >= 1 && np <= WG_MAXP && (int)ys.size() == np && (int)ps.size() == np &&
+                  (int)meta.size() == np * MW, "lora_wgrad_group: 1..16 problems, meta/ps sizes");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.is_cuda(), "lora_wgrad_group: out fp32");
+  const auto dt = xs[0].scalar_type();
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "lora_wgrad_group: bf16/fp16");
+  WgArgs args{};
+  args.out = out.data_ptr<float>();
+  args.sstep = mift_seed_step();
+  int n = 0;
+  for (int i = 0; i < np; ++i) {
+    const at::Tensor& x = xs[i];
+    const at::Tensor& y = ys[i];
+    const int64_t* m = meta.data() + i * MW;
+    TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.scalar_type() == dt,
+                "lora_wgrad_group: x [M,P] with 16-B aligned rows");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "lora_wgrad_group: x 16-B aligned");
+    TORCH_CHECK(y.dim() == 2 && y.is_contiguous() && y.size(1) == 32 && y.size(0) == x.size(0) && y.scalar_type() == dt,
+                "lora_wgrad_group: y [M,32]");
+    const int P = x.size(1), M = x.size(0);
+    TORCH_CHECK(P % 64 == 0, "lora_wgrad_group: P % 64 == 0");
+    const int mode = (int)m[0], nslot = (int)m[1];
+    TORCH_CHECK(mode >= 0 && mode <= 2 && nslot >= 1 && nslot <= WG_MAXS, "lora_wgrad_group: mode / slots");
+    if (M == 0) continue;
+    WgProb& p = args.p[n++];
+    p.X = x.data_ptr();
+    p.Y = y.data_ptr();
+    p.ldx = (int)x.stride(0);
+    p.P = P;
+    p.M = M;
+    p.mode = mode;
+    p.nslot = nslot;
+    p.thr = mift_thr16(ps[i]);
+    p.inv_keep = ps[i] > 0 ? mift_inv_keep(ps[i]) : 1.f;
+    p.seed = (uint64_t)m[2 + 3 * WG_MAXS];
+    for (int si = 0; si < nslot; ++si) {
+      const int qoff = (int)m[2 + 3 * si], rank = (int)m[3 + 3 * si];
+      const int64_t off = m[4 + 3 * si];
+      TORCH_CHECK(qoff >= 0 && rank >= 1 && qoff + rank <= 32, "lora_wgrad_group: slot columns");
+      const int64_t need = mode == 0 ? (int64_t)P * 32 : (int64_t)P * rank;
+      TORCH_CHECK(off >= 0 && off + need <= out.numel(), "lora_wgrad_group: slot range outside out");
+      p.slot[si] = WgSlot{qoff, rank, off};
+    }
+  }
+  args.np = n;
+  if (n == 0) return;
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  if (dt == at::kBFloat16) launch_wgrad<bf16>(args, st);
+  else launch_wgrad<fp16>(args, st);
+}
+
+// one problem (tests, non-arena paths): out fp32, accumulated; mode 0 -> out[P,32];
+// mode 1/2 -> out is a flat arena and the result lands at out[offset:] in dB [P,r] / dA [r,P] layout
 void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, double p, int64_t seed, int64_t mode,
                      int64_t rank, int64_t offset, int64_t qoff) {
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && y.is_contiguous() && y.size(1) == 32, "lora_wgrad: shapes");
-  const int M = x.size(0), P = x.size(1);
-  TORCH_CHECK(y.size(0) == M && P % 64 == 0, "lora_wgrad: P % 64 == 0");
-  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous(), "lora_wgrad: out fp32 contiguous");
-  if (mode == 0) {
-    TORCH_CHECK(out.numel() == (int64_t)P * 32, "lora_wgrad: out [P,32]");
-  } else {
-    TORCH_CHECK(offset + (int64_t)P * rank <= out.numel() && rank <= 32, "lora_wgrad: arena range");
-  }
-  if (M == 0) return;
-  const int ntp = P / 64;
-  int splits = std::max(1, std::min((512 + ntp - 1) / ntp, (M + 127) / 128));
-  int rows = ((M + splits - 1) / splits + 127) / 128 * 128;
-  splits = (M + rows - 1) / rows;
-  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-  const uint32_t thr = mift_thr16(p);
-  const float ik = p > 0 ? mift_inv_keep(p) : 1.f;
-  if (x.scalar_type() == at::kBFloat16)
-    lora_wgrad_kernel<bf16><<<ntp * splits, 256, 0, st>>>((const bf16*)x.data_ptr(), (const bf16*)y.data_ptr(),
-                                                          out.data_ptr<float>() + offset, M, P, (int)x.stride(0), rows,
-                                                          (uint64_t)seed, mift_seed_step(), thr, ik, (int)mode, (int)rank, (int)qoff);
-  else
-    lora_wgrad_kernel<fp16><<<ntp * splits, 256, 0, st>>>((const fp16*)x.data_ptr(), (const fp16*)y.data_ptr(),
-                                                          out.data_ptr<float>() + offset, M, P, (int)x.stride(0), rows,
-                                                          (uint64_t)seed, mift_seed_step(), thr, ik, (int)mode, (int)rank, (int)qoff);
+  TORCH_CHECK(y.is_contiguous() && y.size(1) == 32, "lora_wgrad: shapes");
+  if (mode == 0) TORCH_CHECK(out.numel() == x.size(1) * 32, "lora_wgrad: out [P,32]");
+  std::vector<int64_t> meta(3 + 3 * WG_MAXS, 0);
+  meta[0] = mode;
+  meta[1] = 1;
+  meta[2] = mode == 0 ? 0 : qoff;
+  meta[3] = mode == 0 ? 32 : rank;
+  meta[4] = offset;
+  meta[2 + 3 * WG_MAXS] = seed;
+  mift_lora_wgrad_group(out, {x}, {y}, meta, {p});
 }
 
 // ------------------------------------------------------------ pack_lora_all

@@ -26,9 +26,12 @@ at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at
                              int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale);
 
 // ---- LoRA side path (kernels/lora.hip)
-at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed);
+at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed,
+                          int64_t rows);
 void mift_lora_wgrad(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, double p, int64_t seed, int64_t mode,
                      int64_t rank, int64_t offset, int64_t qoff);
+void mift_lora_wgrad_group(at::Tensor& out, const std::vector<at::Tensor>& xs, const std::vector<at::Tensor>& ys,
+                           const std::vector<int64_t>& meta, const std::vector<double>& ps);
 void mift_pack_lora_all(const at::Tensor& arena, const at::Tensor& table, const at::Tensor& scales, at::Tensor& out,
                         int64_t max_elems);
 
@@ -76,6 +79,7 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
   m.def("layer_norm_fwd_proj", &mift_layer_norm_fwd_proj, "LN fwd + alpha*drop(y)@pw^T -> (y, mean, rstd, proj)"); \
   m.def("mask_proj", &mift_mask_proj, "y = dropout(x) (p>0), proj = alpha*y@pw^T -> (y, proj)"); \
   m.def("lora_wgrad", &mift_lora_wgrad, "out[P,32] += drop(x)^T @ y (tr_b16 split-M MFMA); arena modes"); \
+  m.def("lora_wgrad_group", &mift_lora_wgrad_group, "grouped LoRA weight grads (<= 16 problems, one launch)"); \
   m.def("pack_lora_all", &mift_pack_lora_all, "pack every adapter's 16-bit operands from the fp32 arena"); \
   m.def("attn_fwd", &mift_attn_fwd, "causal flash attention fwd on fused qkv -> (o, lse)"); \
   m.def("attn_bwd", &mift_attn_bwd, "causal flash attention bwd -> dqkv"); \

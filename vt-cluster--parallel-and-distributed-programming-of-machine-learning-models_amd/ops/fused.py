@@ -28,7 +28,7 @@ import os
 import torch
 
 from . import kernels as K
-from .streams import run_side
+from .streams import join as join_side, run_side
 
 # LN fused with the LoRA input projection does LR FMAs per element on the VALU with the [LR,D]
 # operand re-read from cache for every row: a win for one adapter (LR = 8), but for OPT's fused
@@ -36,6 +36,13 @@ from .streams import run_side
 # lora_proj (tools/bench_rowproj.py) — above this many rows, LN and projection run separately.
 # One adapter at OPT's D = 2560 lost too (125 us vs 46 + 40 us); at distilgpt2's D = 768 it is even
 # (17.2 vs 7.6 + 8.9 us) and saves a launch.
+
+
+def _diag_skip(what):
+    """MIFT_DIAG_SKIP=wgrad (diagnostics only, wrong gradients): drop the LoRA weight-grad launches
+    to measure their critical-path cost in a whole step (tools/step_ab.py).  Read per call."""
+    return what in os.environ.get("MIFT_DIAG_SKIP", "").split(",")
+
 _LNPROJ_MAX_ROWS = int(os.environ.get("MIFT_LNPROJ_MAX_ROWS", "8"))
 _LNPROJ_MAX_D = int(os.environ.get("MIFT_LNPROJ_MAX_D", "1024"))
 
@@ -54,7 +61,7 @@ def _mask_proj(g2, p, seed, lo):
     if lo.rows <= _LNPROJ_MAX_ROWS and g2.shape[-1] <= _LNPROJ_MAX_D:
         return K.mask_proj(g2, p, seed, lo.B32t, lo.rows, lo.dt_alpha)
     gz = K.mask_scale(g2, p, seed) if p > 0 else g2
-    return gz, K.lora_proj(gz, lo.B32t, lo.dt_alpha, 0.0, 0)
+    return gz, K.lora_proj(gz, lo.B32t, lo.dt_alpha, 0.0, 0, rows=lo.rows)
 
 _BWD = {0: 0, 1: 4, 2: 5, 3: 6}
 
@@ -66,6 +73,66 @@ def _notify(arena, offsets):
     cb = getattr(arena, "grad_ready", None)
     if cb is not None:
         cb(offsets)
+
+
+class _WgradBatch:
+    """LoRA weight-gradient problems deferred to ONE grouped launch (``lora_wgrad_group``).
+
+    The adapters of a transformer layer queue their dB / dA problems here during backward and
+    the layer's first Function in forward order (``LnLinear``, i.e. the last one in backward)
+    flushes them: one launch per layer instead of two per adapter (each of those paid ~10 us of
+    ramp and tail for 12-50 MB of reads).  The inputs stay referenced until the launch, the DP
+    reducer is notified after it (bucket all-reduces still overlap the next layer's backward),
+    and an end-of-backward callback flushes whatever is left (models without an LnLinear)."""
+    MAX = 16
+
+    def __init__(self):
+        self.arena = None
+        self.xs, self.ys, self.meta, self.ps, self.offs = [], [], [], [], []
+        self.cb = False
+
+    def add(self, arena, x, y, mode, slots, p, seed, offs):
+        if self.arena is not None and (self.arena is not arena or len(self.xs) >= self.MAX):
+            self.flush()
+        self.arena = arena
+        m = [mode, len(slots)]
+        for q, r, o in slots:
+            m += [q, r, o]
+        m += [0, 0, 0] * (4 - len(slots)) + [seed]
+        self.xs.append(x)
+        self.ys.append(y)
+        self.meta += m
+        self.ps.append(p)
+        self.offs += list(offs)
+        if not self.cb:
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._final)
+                self.cb = True
+            except RuntimeError:
+                pass  # not inside backward: flushed by the next flush() call
+
+    def _final(self):
+        self.cb = False
+        if self.xs:
+            self.flush()
+            join_side()
+
+    def flush(self):
+        if not self.xs:
+            return
+        arena, xs, ys, meta, ps, offs = self.arena, self.xs, self.ys, self.meta, self.ps, self.offs
+        self.arena, self.xs, self.ys, self.meta, self.ps, self.offs = None, [], [], [], [], []
+        if not _diag_skip("wgrad"):
+            run_side(xs[0].device, lambda: K.lora_wgrad_group(arena.grad, xs, ys, meta, ps), *xs, *ys)
+        _notify(arena, offs)
+
+
+_WG = _WgradBatch()
+
+
+def flush_wgrads():
+    """Launch the queued LoRA weight-gradient problems now (one grouped kernel)."""
+    _WG.flush()
 
 
 class AdapterOps:
@@ -96,7 +163,7 @@ class AdapterOps:
 
     def forward(self, x, seed, training):
         """T32 = s·dropout(x)·A^T  [M,32] (mask applied in-register, never stored)."""
-        return K.lora_proj(x, self.A32s, 1.0, self.p if training else 0.0, seed)
+        return K.lora_proj(x, self.A32s, 1.0, self.p if training else 0.0, seed, rows=self.rows)
 
     def backward(self, gz, x, T32, seed, training, dT32=None):
         """-> (grads for lora_params() [dA, dB] or [None, None], dT32).
@@ -105,15 +172,10 @@ class AdapterOps:
         r = self.r
         p = self.p if training else 0.0
         if dT32 is None:
-            dT32 = K.lora_proj(gz, self.B32t, self.s, 0.0, 0)        # s·gz·B   [M,32]
-        if self.arena is not None:
-            g, offA, offB = self.arena.grad, self.offA, self.offB
-
-            def wgrad():
-                K.lora_wgrad_into(gz, T32, g, 1, r, offB)              # dB [N,r]
-                K.lora_wgrad_into(x, dT32, g, 2, r, offA, p, seed)     # dA [r,K]
-            run_side(gz.device, wgrad, gz, T32, x, dT32)
-            _notify(self.arena, (offA, offB))
+            dT32 = K.lora_proj(gz, self.B32t, self.s, 0.0, 0, rows=self.rows)  # s·gz·B   [M,32]
+        if self.arena is not None:  # dB [N,r] = gzᵀ·T, dA [r,K] = (drop(x)ᵀ·dT)ᵀ, queued for the layer's launch
+            _WG.add(self.arena, gz, T32, 1, [(0, r, self.offB)], 0.0, 0, (self.offB,))
+            _WG.add(self.arena, x, dT32, 2, [(0, r, self.offA)], p, seed, (self.offA,))
             return [None, None], dT32
         dBf = K.lora_wgrad(gz, T32)
         dAf = K.lora_wgrad(x, dT32, p=p, seed=seed)
@@ -170,23 +232,21 @@ class MultiAdapterOps:
             cat._mpack = (key, (self.A32s, self.B32, self.B32t, self.At32))
 
     def forward(self, x, seed, training):
-        return K.lora_proj(x, self.A32s, 1.0, self.p if training else 0.0, seed)
+        return K.lora_proj(x, self.A32s, 1.0, self.p if training else 0.0, seed, rows=self.rows)
 
     def backward(self, gz, x, T32, seed, training, dT32=None):
         p = self.p if training else 0.0
         if dT32 is None:
-            dT32 = K.lora_proj(gz, self.B32t, 1.0, 0.0, 0)
+            dT32 = K.lora_proj(gz, self.B32t, 1.0, 0.0, 0, rows=self.rows)
         grads = []
-        if self.arena is not None:
-            g, slots = self.arena.grad, self.slots
-
-            def wgrad():
-                for l, n0, n1, q in slots:
-                    K.lora_wgrad_into(gz[:, n0:n1], T32, g, 1, l.lora_r, l._offB, qoff=q)
-                    K.lora_wgrad_into(x, dT32, g, 2, l.lora_r, l._offA, p, seed, qoff=q)
-            run_side(gz.device, wgrad, gz, T32, x, dT32)
-            _notify(self.arena, [o for l, _, _, _ in slots for o in (l._offA, l._offB)])
-            return [None, None] * len(slots), dT32
+        if self.arena is not None:  # per-slot dB on gz's column span; ONE dA problem feeds every slot
+            for l, n0, n1, q in self.slots:
+                _WG.add(self.arena, gz[:, n0:n1], T32, 1, [(q, l.lora_r, l._offB)], 0.0, 0, (l._offB,))
+            for i in range(0, len(self.slots), 4):
+                grp = self.slots[i:i + 4]
+                _WG.add(self.arena, x, dT32, 2, [(q, l.lora_r, l._offA) for l, _, _, q in grp], p, seed,
+                        [l._offA for l, _, _, _ in grp])
+            return [None, None] * len(self.slots), dT32
         dAf = K.lora_wgrad(x, dT32, p=p, seed=seed)
         for l, n0, n1, q in self.slots:
             dBf = K.lora_wgrad(gz[:, n0:n1], T32)
@@ -234,6 +294,7 @@ class LnLinear(torch.autograd.Function):
         gy = _flat(gy.contiguous())
         lg, dT32 = (lo.backward(gy, a, T32, ctx.seed, ctx.training) if lo is not None else (_nones(ctx.nl), None))
         da = _dgrad(gy, lin, lo, dT32, ctx.seed, ctx.training)
+        _WG.flush()  # the layer's first op in forward order: its adapters' weight grads, one launch
         dx, _, _, _ = K.layer_norm_bwd(da, x2, ln_w, mean, rstd)
         return (dx.view(ctx.shp), None, None, None, None, None, None, *lg)
 

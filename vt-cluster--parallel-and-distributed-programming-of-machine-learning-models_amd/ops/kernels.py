@@ -3,8 +3,6 @@
 Every wrapper launches on torch's current HIP stream.  CPU callers use
 ``mift.ops.reference`` instead (see ``mift.ops.dispatch``).
 """
-import os
-
 import torch
 
 from .dispatch import C
@@ -25,18 +23,9 @@ def gemm(a, b, bias=None, a2=None, b2=None, act=0, aux=None, residual=None, drop
     return (y, pre) if want_preact else y
 
 
-# Without dropout the projection is a plain tall-skinny GEMM: at OPT-2.7B sizes (M*K >= ~50M
-# elements) hipBLASLt streams x at ~5.6 TB/s against lora_proj's ~4 TB/s (22 vs 30 us at 24576 x
-# 2560, 68 vs 105 us at 24576 x 7680); below that lora_proj wins (14 vs 20 us at 8192 x 3072).
-_PROJ_BLAS_MIN = int(os.environ.get("MIFT_PROJ_BLAS_MIN", str(48 << 20)))
-
-
-def lora_proj(x, w32, alpha=1.0, p=0.0, seed=0):
-    """[M,32] = alpha * dropout(x) @ w32.T   (w32: [32, K])."""
-    if p == 0.0 and x.dim() == 2 and x.shape[0] * x.shape[1] >= _PROJ_BLAS_MIN:
-        y = torch.mm(x, w32.t())
-        return y if alpha == 1.0 else y.mul_(alpha)
-    return C().lora_proj(x, w32, float(alpha), float(p), int(seed))
+def lora_proj(x, w32, alpha=1.0, p=0.0, seed=0, rows=32):
+    """[M,32] = alpha * dropout(x) @ w32.T   (w32: [32, K]; only its first ``rows`` rows may be non-zero)."""
+    return C().lora_proj(x, w32, float(alpha), float(p), int(seed), int(rows))
 
 
 def lora_wgrad(x, y32, out=None, p=0.0, seed=0):
@@ -46,6 +35,12 @@ def lora_wgrad(x, y32, out=None, p=0.0, seed=0):
         out = torch.zeros(x.shape[1], 32, dtype=torch.float32, device=x.device)
     C().lora_wgrad(x, y32, out, float(p), int(seed), 0, 32, 0, 0)
     return out
+
+
+def lora_wgrad_group(out, xs, ys, meta, ps):
+    """Grouped weight grads (one launch, <= 16 problems) into the flat fp32 ``out``;
+    meta: per problem [mode, nslot, (qoff, rank, offset) x 4, seed] (csrc/kernels/lora.hip)."""
+    C().lora_wgrad_group(out, list(xs), list(ys), [int(v) for v in meta], [float(v) for v in ps])
 
 
 def lora_wgrad_into(x, y32, arena_grad, mode, rank, offset, p=0.0, seed=0, qoff=0):
