@@ -94,3 +94,20 @@ def test_lmhead_large_logits_stable():
     assert torch.isfinite(hx.grad).all()
     assert float(loss) == pytest.approx(float(rl), rel=3e-3)
     assert float((hx.grad.float() - rg).norm() / rg.norm()) < 3e-2
+
+
+@pytest.mark.parametrize("V,dtype,ignore", [(50257, torch.bfloat16, -100), (50272, torch.float16, 1)])
+def test_lmhead_in_kernel_shift(V, dtype, ignore):
+    """shift = S (labels passed unshifted, the causal shift done by the kernels) equals the
+    host-shifted labels, loss and gradient, incl. OPT's pad-id ignore index."""
+    from mift.models.base import shift_labels
+    S = 128
+    h, ln, W, lab, Vp = _case(V, dtype, ignore, M=4 * S)
+    gup = 0.5
+    ids = lab.view(4, S)
+    hx = h.clone().requires_grad_(True)
+    loss = F.lm_head_xent(hx, ln, W, ids, V, ignore, need_grad=True, w_kn=W.t().contiguous(), shift=S)
+    (loss * gup).backward()
+    rl, rg, _ = _ref(h, ln, W, shift_labels(ids, ignore).reshape(-1), V, ignore, gup)
+    assert float(loss) == pytest.approx(float(rl), rel=3e-3)
+    assert float((hx.grad.float() - rg).norm() / rg.norm()) < 3e-2

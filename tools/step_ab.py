@@ -6,6 +6,7 @@ under its own environment (kernel knobs are read when the step's graph is captur
 their steps are timed in interleaved blocks; the medians are compared.
 
   python tools/step_ab.py "MIFT_GEMM_GROUP=0" "MIFT_GEMM_GROUP=4" [--blocks 6 --steps 10]
+(AB_LORA_P=x / AB_MODEL_PDROP=x: diagnostic arms with other dropout rates)
 """
 import argparse
 import json
@@ -47,7 +48,12 @@ def main():
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         model = build_causal_lm(a.model, dtype=torch.bfloat16, device=ctx.device, seed=0)
-        L.inject(model, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["c_attn", "c_proj"],
+        # diagnostics only: AB_LORA_P / AB_MODEL_PDROP change the dropout rates of this arm
+        lp = float(env.get("AB_LORA_P", 0.05))
+        if "AB_MODEL_PDROP" in env:
+            for k in ("attn_pdrop", "resid_pdrop", "embd_pdrop"):
+                setattr(model.config, k, float(env["AB_MODEL_PDROP"]))
+        L.inject(model, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=lp, target_modules=["c_attn", "c_proj"],
                                      base_model_name_or_path=a.model))
         n = per_rank * (a.blocks * a.steps + 4)
         ds = synthetic_openwebtext(n, seq, model.config.vocab_size, model.config.pad_token_id, seed=1234,

@@ -73,7 +73,16 @@ struct LmArgs {
   int gpc;                // groups per split-K chunk
   float* partial;         // [S][M][N] fp32 split-K slabs
   int dbg;                // MIFT_LM_DBG (diagnostics only): bit 0 = skip the E store
+  int shift;              // > 0: labels are the UNSHIFTED [B*S] ids, S = shift (see lm_label)
 };
+
+// Target of row `row`: with shift = S the labels tensor holds the unshifted ids and row r's target
+// is ids[r + 1] within its sequence (none for a sequence's last position) — the causal-LM shift done
+// in the kernels instead of by two extra tensor ops per step.
+MIFT_HD int64_t lm_label(const int64_t* labels, int row, int shift) {
+  if (shift <= 0) return labels[row];
+  return (row % shift == shift - 1) ? (int64_t)-1 : labels[row + 1];
+}
 
 struct EpiArgs {
   LmArgs lm;
@@ -568,7 +577,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     // labels first: their load latency hides under the max pass (they are consumed after a barrier)
     int64_t labs[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) labs[i] = lm.labels[min(m0 + wm * WM + i * 16 + fr, M - 1)];
+    for (int i = 0; i < TM; ++i) labs[i] = lm_label(lm.labels, min(m0 + wm * WM + i * 16 + fr, M - 1), lm.shift);
     const bool full = n0 + BN <= V;  // block-uniform: only the last column tile holds padding columns
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -953,7 +962,7 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
 // ---- LM head: loss from the forward's tile statistics (one wave per row) ----
 __global__ __launch_bounds__(256) void lmhead_lse_kernel(const float2* __restrict__ stats, int ntn,
                                                          const float* __restrict__ zlab,
-                                                         const int64_t* __restrict__ labels, int V, int M,
+                                                         const int64_t* __restrict__ labels, int V, int M, int shift,
                                                          float* __restrict__ lse, float* __restrict__ loss) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -968,7 +977,7 @@ __global__ __launch_bounds__(256) void lmhead_lse_kernel(const float2* __restric
   if (lane == 0) {
     const float l = m + __logf(s);
     lse[row] = l;
-    const int64_t lab = labels[row];
+    const int64_t lab = lm_label(labels, row, shift);
     loss[row] = (lab >= 0 && lab < V) ? l - zlab[row] : 0.f;
   }
 }
@@ -977,7 +986,7 @@ __global__ __launch_bounds__(256) void lmhead_lse_kernel(const float2* __restric
 template <typename T>
 __global__ __launch_bounds__(256) void lmhead_reduce_kernel(const float* __restrict__ partial, int S, int M, int N,
                                                             const T* __restrict__ w, int ldw,
-                                                            const int64_t* __restrict__ labels, int V,
+                                                            const int64_t* __restrict__ labels, int V, int shift,
                                                             const float* __restrict__ gscale, T* __restrict__ out) {
   const size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;  // one 8-column chunk
   const int cpr = N / 8;
@@ -994,7 +1003,7 @@ __global__ __launch_bounds__(256) void lmhead_reduce_kernel(const float* __restr
     float4 a = p[0], b = p[1];
     acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w; acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
   }
-  const int64_t lab = labels[row];
+  const int64_t lab = lm_label(labels, row, shift);
   if (lab >= 0 && lab < V) {  // dX = g·(softmax·W - W[label]); rows without a target get 0
     float wv[8];
     load8<T>(w + (size_t)lab * ldw + c8, wv);
@@ -1009,14 +1018,15 @@ __global__ __launch_bounds__(256) void lmhead_reduce_kernel(const float* __restr
 }
 
 template <typename T>
-std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int V) {
+std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int V,
+                                        int shift) {
   const int M = a.size(0), K = a.size(1), N = w.size(0);
   constexpr int BM = 256, BN = 256;
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   auto E = at::empty({M, N}, a.options());
   auto f32 = a.options().dtype(at::kFloat);
   auto stats = at::empty({M, ntn, 2}, f32);
-  auto zlab = at::zeros({M}, f32);
+  auto zlab = at::empty({M}, f32);  // written for every row with a target; read only for those
   auto lse = at::empty({M}, f32);
   auto loss = at::empty({M}, f32);
   EpiArgs ep{};
@@ -1026,6 +1036,7 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   ep.lm.stats = reinterpret_cast<float2*>(stats.data_ptr<float>());
   ep.lm.zlab = zlab.data_ptr<float>();
   ep.lm.ntn = ntn;
+  ep.lm.shift = shift;
   if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);
   {
     const char* g = getenv("MIFT_GEMM_GROUP");  // row-panel order measured best for the fused head
@@ -1054,13 +1065,13 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
                      (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
   hipLaunchKernelGGL(lmhead_lse_kernel, dim3((M + 3) / 4), dim3(256), 0, st,
                      reinterpret_cast<const float2*>(stats.data_ptr<float>()), ntn, zlab.data_ptr<float>(),
-                     labels.data_ptr<int64_t>(), V, M, lse.data_ptr<float>(), loss.data_ptr<float>());
+                     labels.data_ptr<int64_t>(), V, M, shift, lse.data_ptr<float>(), loss.data_ptr<float>());
   return {E, stats, lse, loss, zlab};
 }
 
 template <typename T>
 at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
-                             int V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale) {
+                             int V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale, int shift) {
   const int M = E.size(0), K = E.size(1), N = wt.size(0);
   const int ntn_f = stats.size(1);
   constexpr int BM = 256, BN = 256;
@@ -1084,6 +1095,7 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   ep.lm.ntn = ntn_f;
   ep.lm.gpc = gpc;
   ep.lm.partial = partial.data_ptr<float>();
+  ep.lm.shift = shift;
   SkArgs sk{};
   auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
   static bool attr = false;
@@ -1098,16 +1110,18 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   const size_t chunks = (size_t)M * (N / 8);
   hipLaunchKernelGGL(lmhead_reduce_kernel<T>, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st,
                      partial.data_ptr<float>(), S, M, N, (const T*)w.data_ptr(), (int)w.stride(0),
-                     labels.data_ptr<int64_t>(), V, gscale.data_ptr<float>(), (T*)out.data_ptr());
+                     labels.data_ptr<int64_t>(), V, shift, gscale.data_ptr<float>(), (T*)out.data_ptr());
   return out;
 }
 
 }  // namespace
 
 // Fused LM head + cross-entropy forward: a = LN(h) [M,K], w = tied embedding [V_pad,K],
-// labels [M] int64 (already shifted; ignore -> any value outside [0, V)).
+// labels [M] int64 (ignore -> any value outside [0, V)): the targets themselves (shift = 0), or the
+// unshifted ids of sequences of length shift (row r's target = ids[r + 1] inside its sequence).
 // -> (E [M,V_pad] = exp(z - m_tile) 16-bit, stats [M, V_pad/256, 2] (m, s), lse [M], loss [M], zlab [M]).
-std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V) {
+std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V,
+                                        int64_t shift) {
   TORCH_CHECK(a.is_cuda() && w.is_cuda() && labels.is_cuda(), "lmhead_fwd: GPU tensors");
   TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1), "lmhead_fwd: a [M,K], w [V_pad,K]");
   TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && a.size(1) % 64 == 0, "lmhead_fwd: K-contiguous, K % 64 == 0");
@@ -1115,17 +1129,19 @@ std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w
   TORCH_CHECK(w.size(0) % 8 == 0 && V <= w.size(0) && w.size(0) - V < 256, "lmhead_fwd: V_pad % 8, V_pad - V < 256");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == a.size(0),
               "lmhead_fwd: int64 labels [M]");
+  TORCH_CHECK(shift >= 0 && (shift == 0 || a.size(0) % shift == 0), "lmhead_fwd: rows must be whole sequences");
   TORCH_CHECK(a.scalar_type() == w.scalar_type(), "lmhead_fwd: dtype mismatch");
-  if (a.scalar_type() == at::kBFloat16) return lmhead_fwd_impl<bf16>(a, w, labels, (int)V);
+  if (a.scalar_type() == at::kBFloat16) return lmhead_fwd_impl<bf16>(a, w, labels, (int)V, (int)shift);
   TORCH_CHECK(a.scalar_type() == at::kHalf, "lmhead_fwd: bf16/fp16");
-  return lmhead_fwd_impl<fp16>(a, w, labels, (int)V);
+  return lmhead_fwd_impl<fp16>(a, w, labels, (int)V, (int)shift);
 }
 
 // Backward of the fused head: dX [M,N] = g·(softmax - onehot)·W without materialising dlogits.
 // E / stats / lse from mift_lmhead_fwd; wt = Wᵀ [N, V_pad] (K-contiguous), w = W [V_pad, N];
 // gscale: 1-element fp32 device tensor (upstream gradient, e.g. loss_scale / tokens).
 at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
-                             int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale) {
+                             int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale,
+                             int64_t shift) {
   TORCH_CHECK(E.is_cuda() && wt.is_cuda() && w.is_cuda(), "lmhead_dgrad: GPU tensors");
   TORCH_CHECK(E.dim() == 2 && wt.dim() == 2 && wt.size(1) == E.size(1), "lmhead_dgrad: E [M,V_pad], wt [N,V_pad]");
   TORCH_CHECK(E.stride(1) == 1 && wt.stride(1) == 1 && E.size(1) % 64 == 0, "lmhead_dgrad: V_pad % 64 == 0");
@@ -1139,9 +1155,9 @@ at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at
   TORCH_CHECK(lse.numel() == E.size(0) && gscale.numel() >= 1 && gscale.scalar_type() == at::kFloat,
               "lmhead_dgrad: lse [M], fp32 gscale");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == E.size(0), "lmhead_dgrad: labels");
-  if (E.scalar_type() == at::kBFloat16) return lmhead_dgrad_impl<bf16>(E, wt, w, labels, (int)V, stats, lse, gscale);
+  if (E.scalar_type() == at::kBFloat16) return lmhead_dgrad_impl<bf16>(E, wt, w, labels, (int)V, stats, lse, gscale, (int)shift);
   TORCH_CHECK(E.scalar_type() == at::kHalf, "lmhead_dgrad: bf16/fp16");
-  return lmhead_dgrad_impl<fp16>(E, wt, w, labels, (int)V, stats, lse, gscale);
+  return lmhead_dgrad_impl<fp16>(E, wt, w, labels, (int)V, stats, lse, gscale, (int)shift);
 }
 
 // out = epi(a @ b^T [+ a2 @ b2^T]).  a:[M,K], b:[N,K] (K-contiguous, K%64==0).

@@ -21,9 +21,11 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                                      const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed);
 
 // ---- K2/K7 fused LM head + cross-entropy (kernels/gemm.hip, EPI 1/2)
-std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V);
+std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V,
+                                        int64_t shift);
 at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
-                             int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale);
+                             int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale,
+                             int64_t shift);
 
 // ---- LoRA side path (kernels/lora.hip)
 at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed,

@@ -131,14 +131,15 @@ class GPT2Block(nn.Module):
         cfg = self.cfg
         B, S, d = h.shape
         H, hd = self.attn.n_head, self.attn.head_dim
-        qkv = F.ln_linear(h, self.ln_1, self.attn.c_attn, seeds["lora_attn"], training)
+        link = F.ResidualLink()  # residual grad of h enters the LN backward (no separate add kernel)
+        qkv = F.ln_linear(h, self.ln_1, self.attn.c_attn, seeds["lora_attn"], training, link=link)
         if attn is not None:
             o = attn(qkv)
         else:
             o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5, dropout_p=cfg.attn_pdrop if training else 0.0,
                                  seed=seeds["attn"], kv_len=kv_len)
         h = F.linear_residual(o, h, self.attn.c_proj, cfg.resid_pdrop, seeds["attn_out"], seeds["lora_proj"],
-                              training)
+                              training, link=link)
         return F.mlp(h, self.ln_2, self.mlp.c_fc, self.mlp.c_proj, act=1, p=cfg.resid_pdrop, seed=seeds["mlp_out"],
                      seed_l1=0, seed_l2=seeds["lora_mlp"], training=training)
 

@@ -39,10 +39,10 @@ def fused_forward(model, input_ids, attention_mask, labels, hidden_states, reduc
         return {"hidden_states": h}
     w_nk, w_kn = model.lm_weight_padded(transposed=labels is not None and torch.is_grad_enabled())
     if labels is not None:
-        sl = shift_labels(labels)
-        loss_sum = F.lm_head_xent(h, model.transformer.ln_f, w_nk, sl, cfg.vocab_size, -100,
-                                  need_grad=torch.is_grad_enabled(), w_kn=w_kn)
-        ntok = (sl != -100).sum()
+        # causal shift inside the head kernels (shift = S); token count only for a mean
+        loss_sum = F.lm_head_xent(h, model.transformer.ln_f, w_nk, labels, cfg.vocab_size, -100,
+                                  need_grad=torch.is_grad_enabled(), w_kn=w_kn, shift=labels.shape[-1])
+        ntok = (labels[:, 1:] != -100).sum() if reduction == "mean" else None
         loss = loss_sum / ntok.clamp(min=1) if reduction == "mean" else loss_sum
         return {"loss": loss, "logits": None, "ntokens": ntok}
     logits = F.lm_head_logits(h, model.transformer.ln_f, w_nk, cfg.vocab_size)

@@ -157,8 +157,10 @@ class OPTDecoderLayer(nn.Module):
         B, S, d = h.shape
         at = self.self_attn
         H, hd = at.n_head, at.head_dim
+        link = None
         if at.qkv.fusable():
-            qkv = F.ln_linear(h, self.self_attn_layer_norm, at.qkv, seeds["lora_attn"], training)
+            link = F.ResidualLink()  # residual grad of h enters the LN backward (no separate add)
+            qkv = F.ln_linear(h, self.self_attn_layer_norm, at.qkv, seeds["lora_attn"], training, link=link)
         else:  # adapters too wide for one shared K-extension: three projections
             qkv = torch.cat([F.ln_linear(h, self.self_attn_layer_norm, l, seeds["lora_attn"], training)
                              for l in (at.q_proj, at.k_proj, at.v_proj)], -1)
@@ -168,7 +170,8 @@ class OPTDecoderLayer(nn.Module):
             o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5,
                                  dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"],
                                  kv_len=kv_len)
-        h = F.linear_residual(o, h, at.out_proj, cfg.dropout, seeds["attn_out"], seeds["lora_proj"], training)
+        h = F.linear_residual(o, h, at.out_proj, cfg.dropout, seeds["attn_out"], seeds["lora_proj"], training,
+                              link=link)
         return F.mlp(h, self.final_layer_norm, self.fc1, self.fc2, act=2, p=cfg.dropout, seed=seeds["mlp_out"],
                      seed_l1=seeds["lora_fc1"], seed_l2=seeds["lora_fc2"], training=training)
 
@@ -293,10 +296,11 @@ class OPTForCausalLM(CausalLMBase):
             return {"hidden_states": h}
         w_nk, w_kn = self.lm_weight_padded(transposed=labels is not None and torch.is_grad_enabled())
         if labels is not None:
-            sl = shift_labels(labels, ignore_index)
-            loss_sum = F.lm_head_xent(h, dec.final_layer_norm, w_nk, sl, cfg.vocab_size, ignore_index,
-                                      need_grad=torch.is_grad_enabled(), w_kn=w_kn)
-            ntok = (sl != ignore_index).sum()
+            # the causal shift happens inside the head kernels (shift = S); the token count only
+            # when a mean is asked for (the trainer normalises by its precomputed global count)
+            loss_sum = F.lm_head_xent(h, dec.final_layer_norm, w_nk, labels, cfg.vocab_size, ignore_index,
+                                      need_grad=torch.is_grad_enabled(), w_kn=w_kn, shift=labels.shape[-1])
+            ntok = (labels[:, 1:] != ignore_index).sum() if reduction == "mean" else None
             loss = loss_sum / ntok.clamp(min=1) if reduction == "mean" else loss_sum
             return {"loss": loss, "logits": None, "ntokens": ntok}
         return {"loss": None, "logits": F.lm_head_logits(h, dec.final_layer_norm, w_nk, cfg.vocab_size)}

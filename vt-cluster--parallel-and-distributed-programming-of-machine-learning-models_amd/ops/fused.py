@@ -271,9 +271,22 @@ def _nones(n):
 
 
 # ---------------------------------------------------------------------------
+class ResidualLink:
+    """Carries the residual-stream gradient from ``linear_residual``'s backward to the
+    ``ln_linear`` that read the same hidden state: h feeds both (LN -> qkv, and the residual
+    add), and instead of autograd summing the two gradients with a separate add kernel, the
+    residual part enters ``layer_norm_bwd`` as its ``dres`` operand (reverse order is
+    guaranteed: the residual Function consumes the attention output, which depends on the LN
+    branch)."""
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
 class LnLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, ln_w, ln_b, lin, eps, lora_seed, training, *lparams):
+    def forward(ctx, x, ln_w, ln_b, lin, eps, lora_seed, training, link, *lparams):
         shp = x.shape
         x2 = _flat(x.contiguous())
         lo = lin.lora_ops(x.dtype) if lparams else None
@@ -285,6 +298,7 @@ class LnLinear(torch.autograd.Function):
         y = K.gemm(a, lin.w_nk(), lin.bias, T32, lo.B32 if lo else None)
         ctx.save_for_backward(x2, a, mean, rstd, ln_w, T32)
         ctx.lin, ctx.lo, ctx.seed, ctx.training, ctx.shp, ctx.nl = lin, lo, lora_seed, training, shp, len(lparams)
+        ctx.link = link
         return y.view(*shp[:-1], y.shape[-1])
 
     @staticmethod
@@ -293,20 +307,26 @@ class LnLinear(torch.autograd.Function):
         lin, lo = ctx.lin, ctx.lo
         gy = _flat(gy.contiguous())
         lg, dT32 = (lo.backward(gy, a, T32, ctx.seed, ctx.training) if lo is not None else (_nones(ctx.nl), None))
-        da = _dgrad(gy, lin, lo, dT32, ctx.seed, ctx.training)
         _WG.flush()  # the layer's first op in forward order: its adapters' weight grads, one launch
-        dx, _, _, _ = K.layer_norm_bwd(da, x2, ln_w, mean, rstd)
-        return (dx.view(ctx.shp), None, None, None, None, None, None, *lg)
+        gres = ctx.link.g if ctx.link is not None else None
+        if ctx.link is not None:
+            ctx.link.g = None
+        if not ctx.needs_input_grad[0]:
+            # e.g. the first block, fed by the frozen embedding: no dX -> no dgrad GEMM, no LN backward
+            return (None, None, None, None, None, None, None, None, *lg)
+        da = _dgrad(gy, lin, lo, dT32, ctx.seed, ctx.training)
+        dx, _, _, _ = K.layer_norm_bwd(da, x2, ln_w, mean, rstd, dres=None if gres is None else _flat(gres.contiguous()))
+        return (dx.view(ctx.shp), None, None, None, None, None, None, None, *lg)
 
 
-def ln_linear(x, ln, lin, lora_seed=0, training=True):
-    return LnLinear.apply(x, ln.weight, ln.bias, lin, ln.eps, lora_seed, training, *lin.lora_params())
+def ln_linear(x, ln, lin, lora_seed=0, training=True, link=None):
+    return LnLinear.apply(x, ln.weight, ln.bias, lin, ln.eps, lora_seed, training, link, *lin.lora_params())
 
 
 # ---------------------------------------------------------------------------
 class LinearResidual(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, h, lin, p, seed, lora_seed, training, *lparams):
+    def forward(ctx, x, h, lin, p, seed, lora_seed, training, link, *lparams):
         shp = h.shape
         x2 = _flat(x.contiguous())
         h2 = _flat(h.contiguous())
@@ -316,7 +336,7 @@ class LinearResidual(torch.autograd.Function):
         y = K.gemm(x2, lin.w_nk(), lin.bias, T32, lo.B32 if lo else None, residual=h2, dropout_p=pp, seed=seed)
         ctx.save_for_backward(x2, T32)
         ctx.lin, ctx.lo, ctx.p, ctx.seed, ctx.lseed = lin, lo, pp, seed, lora_seed
-        ctx.training, ctx.xshp, ctx.nl = training, x.shape, len(lparams)
+        ctx.training, ctx.xshp, ctx.nl, ctx.link = training, x.shape, len(lparams), link
         return y.view(shp)
 
     @staticmethod
@@ -331,11 +351,14 @@ class LinearResidual(torch.autograd.Function):
             gz = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
             lg, dT32 = _nones(ctx.nl), None
         dx = _dgrad(gz, lin, lo, dT32, ctx.lseed, ctx.training)
-        return (dx.view(ctx.xshp), gh, None, None, None, None, None, *lg)
+        gres = gh
+        if ctx.link is not None and ctx.needs_input_grad[1]:
+            ctx.link.g, gres = gh, None  # delivered through the linked ln_linear's LN backward
+        return (dx.view(ctx.xshp), gres, None, None, None, None, None, None, *lg)
 
 
-def linear_residual(x, h, lin, p, seed, lora_seed=0, training=True):
-    return LinearResidual.apply(x, h, lin, p, seed, lora_seed, training, *lin.lora_params())
+def linear_residual(x, h, lin, p, seed, lora_seed=0, training=True, link=None):
+    return LinearResidual.apply(x, h, lin, p, seed, lora_seed, training, link, *lin.lora_params())
 
 
 # ---------------------------------------------------------------------------
@@ -411,7 +434,7 @@ class LMHeadXent(torch.autograd.Function):
     hipBLASLt dgrad) for A/B measurements."""
 
     @staticmethod
-    def forward(ctx, h, ln_w, ln_b, eps, w_nk, labels, V, ignore_index, need_grad, w_kn):
+    def forward(ctx, h, ln_w, ln_b, eps, w_nk, labels, V, ignore_index, need_grad, w_kn, shift):
         shp = h.shape
         h2 = _flat(h.contiguous())
         a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
@@ -419,19 +442,21 @@ class LMHeadXent(torch.autograd.Function):
         if ignore_index >= 0:  # e.g. OPT ignores the pad id, a real vocabulary entry
             lab = torch.where(lab == ignore_index, torch.full_like(lab, -1), lab)
         lab = lab.contiguous()
-        E, stats, lse, loss_rows, _ = K.lmhead_fwd(a, w_nk, lab, V)
+        E, stats, lse, loss_rows, _ = K.lmhead_fwd(a, w_nk, lab, V, shift)
         if need_grad:
             ctx.save_for_backward(h2, mean, rstd, ln_w, E, stats, lse, lab)
-        ctx.shp, ctx.w_nk, ctx.w_kn, ctx.V = shp, w_nk, w_kn, V
+        ctx.shp, ctx.w_nk, ctx.w_kn, ctx.V, ctx.shift = shp, w_nk, w_kn, V, shift
         return loss_rows.sum()
 
     @staticmethod
     def backward(ctx, g):
         h2, mean, rstd, ln_w, E, stats, lse, lab = ctx.saved_tensors
         w_kn = ctx.w_kn if ctx.w_kn is not None else ctx.w_nk.t().contiguous()
-        da = K.lmhead_dgrad(E, w_kn, ctx.w_nk, lab, ctx.V, stats, lse, g.reshape(1).float())
+        g1 = g.reshape(1)
+        da = K.lmhead_dgrad(E, w_kn, ctx.w_nk, lab, ctx.V, stats, lse, g1 if g1.dtype == torch.float32 else g1.float(),
+                            ctx.shift)
         dh, _, _, _ = K.layer_norm_bwd(da, h2, ln_w, mean, rstd)
-        return dh.view(ctx.shp), None, None, None, None, None, None, None, None, None
+        return dh.view(ctx.shp), None, None, None, None, None, None, None, None, None, None
 
 
 class LMHeadXentBlas(torch.autograd.Function):
@@ -482,10 +507,16 @@ def _xent_chunk(M, Vp):
     return M if c <= 0 or c >= M else c
 
 
-def lm_head_xent(h, ln, w_nk, labels, V, ignore_index=-100, need_grad=True, w_kn=None):
+def lm_head_xent(h, ln, w_nk, labels, V, ignore_index=-100, need_grad=True, w_kn=None, shift=0):
+    """Summed token CE.  ``labels``: per-row targets (shift = 0) or, with ``shift = S``, the unshifted
+    [B, S] ids (row r's target is ids[r + 1] within its sequence, none at a sequence's end)."""
     if os.environ.get("MIFT_LMHEAD", "fused") == "blas":
+        if shift:
+            from ..models.base import shift_labels
+            labels = shift_labels(labels.reshape(-1, shift), ignore_index)
         return LMHeadXentBlas.apply(h, ln.weight, ln.bias, ln.eps, w_nk, labels, V, ignore_index, need_grad)
-    return LMHeadXent.apply(h, ln.weight, ln.bias, ln.eps, w_nk, labels, V, ignore_index, need_grad, w_kn)
+    return LMHeadXent.apply(h, ln.weight, ln.bias, ln.eps, w_nk, labels, V, ignore_index, need_grad, w_kn,
+                            int(shift))
 
 
 def lm_head_logits(h, ln, w_nk, V):

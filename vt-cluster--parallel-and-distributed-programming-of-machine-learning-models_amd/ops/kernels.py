@@ -74,14 +74,15 @@ def pack_lora(A, B, a_scale, dtype):
     return C().pack_lora(A, B, float(a_scale), dtype)
 
 
-def lmhead_fwd(a, w_nk, labels, V):
-    """Fused LM head + CE forward -> (E, stats, lse, loss_rows, zlab); labels outside [0, V) ignored."""
-    return C().lmhead_fwd(a, w_nk, labels, int(V))
+def lmhead_fwd(a, w_nk, labels, V, shift=0):
+    """Fused LM head + CE forward -> (E, stats, lse, loss_rows, zlab); labels outside [0, V) ignored.
+    ``shift = S``: labels are the unshifted ids of length-S sequences (row r's target is ids[r + 1])."""
+    return C().lmhead_fwd(a, w_nk, labels, int(V), int(shift))
 
 
-def lmhead_dgrad(E, w_kn, w_nk, labels, V, stats, lse, gscale):
+def lmhead_dgrad(E, w_kn, w_nk, labels, V, stats, lse, gscale, shift=0):
     """dX = g·(softmax - onehot)·W from the forward's E / tile stats (no dlogits)."""
-    return C().lmhead_dgrad(E, w_kn, w_nk, labels, int(V), stats, lse, gscale)
+    return C().lmhead_dgrad(E, w_kn, w_nk, labels, int(V), stats, lse, gscale, int(shift))
 
 
 def xent(logits, labels, V, ignore_index=-100, write_grad=True):

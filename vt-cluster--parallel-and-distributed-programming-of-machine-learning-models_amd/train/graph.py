@@ -72,17 +72,20 @@ class GraphedStep:
         """The captured region: forward + backward of every micro-batch."""
         tr, model = self.tr, self.tr.model
         C = _C()
-        ent["loss"].zero_()
-        gscale = tr.opt.loss_scale_t * self.inv_ntok
+        # the scaled upstream gradient seeds backward directly (no ones-fill + multiply kernels)
+        gscale = (tr.opt.loss_scale_t * self.inv_ntok).reshape(())
         for i in range(n):
             C.set_seed_step(ent["steps_t"][i:i + 1])
             mb = ent["static"][i]
             out = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"], labels=mb["labels"],
                         reduction="sum", return_logits=False)
             loss_sum = out["loss"].float()
-            (loss_sum * gscale).backward()
+            loss_sum.backward(gscale)
             streams.join()
-            ent["loss"].add_(loss_sum.detach())
+            if i == 0:
+                ent["loss"].copy_(loss_sum.detach())
+            else:
+                ent["loss"].add_(loss_sum.detach())
         C.set_seed_step(None)
 
     def _capture(self, sig, mbs):

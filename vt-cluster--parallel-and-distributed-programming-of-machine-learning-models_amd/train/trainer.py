@@ -204,7 +204,7 @@ class Trainer:
                     out = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"],
                                 labels=mb["labels"], reduction="sum", return_logits=False)
                 loss_sum = out["loss"].float()
-                (loss_sum * gscale).backward()
+                loss_sum.backward(gscale.reshape(()))
             loss_acc += loss_sum.detach()
             maybe_inject(self.rank, self.global_step + 1, "micro")
         res = self._finish_step(loss_acc, ntok)
