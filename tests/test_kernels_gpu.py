@@ -323,7 +323,7 @@ def test_gemm_ext_masked():
     torch.testing.assert_close(out.float(), exp, atol=5e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("M,N,K", [(4096, 2560, 2560), (1000, 2304, 768), (8192, 768, 3072), (777, 1000, 320),
                                    (300, 520, 64)])
 def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):

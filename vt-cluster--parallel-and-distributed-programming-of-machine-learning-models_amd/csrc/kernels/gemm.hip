@@ -241,8 +241,15 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     for (int s = 0; s < NBUF - 1; ++s)
       if (s < nk) stage(s, (kb + s) * BK);
     for (int kt = 0; kt < nk; ++kt) {
-      // tile kt landed <=> at most (#tiles issued after kt) * PER_STAGE pieces outstanding
-      if constexpr (NBUF >= 3) {
+      // tile kt landed <=> at most (#tiles issued after kt) * PER_STAGE pieces outstanding:
+      // min(NBUF - 2, nk - 1 - kt) tiles were issued after it (counted, never drained to 0 early)
+      if constexpr (NBUF >= 4) {
+        const int after = min(NBUF - 2, nk - 1 - kt);
+        if (after >= 2) wait_vmcnt<2 * PER_STAGE>();
+        else if (after == 1) wait_vmcnt<PER_STAGE>();
+        else wait_vmcnt<0>();
+        static_assert(NBUF <= 4 && 2 * PER_STAGE < 64, "deeper rings need more wait cases");
+      } else if constexpr (NBUF == 3) {
         if (kt + 1 < nk) wait_vmcnt<PER_STAGE>();
         else wait_vmcnt<0>();
       } else {
@@ -920,6 +927,11 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
 //      ragged waves: N=768 gives 512 tiles = exactly one wave of 2x256 slots (128x128: 384)
 //   8: 256x256, 8 waves (2x4), phased schedule (mainloop8: 4 phases per k-tile, staggered wave
 //      rows, counted vmcnt across barriers, setprio MFMA clusters)
+//   9: 128x192, 8 waves (2x4, wave tile 64x48), 2-stage ring (80 KiB -> two blocks = 16 waves per
+//      CU): the wide-N distilgpt2 shapes (N = 2304 / 3072, K = 768) ran 20-25 % faster than 128x96 /
+//      128x128 (c_fc fwd 52.6 vs 63.5 us, c_attn fwd 37.2 vs 48.9, c_proj dgrad 62.3 vs 75.7);
+//      with fewer than two tiles per CU (N = 768) it lost up to 2x.  Deeper rings (3-4 stages, one
+//      block per CU) lost 30-50 % on every distilgpt2 shape (tools/bench_kernels.py --only dgpt).
 template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
@@ -936,6 +948,7 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
     if ((K >= 1024 && n256 >= 128) || n256 >= 2048) tile = 8;
     else if (K >= 4096 && t128 >= 128) tile = 6;
+    else if (N % 192 == 0 && (long)((M + 127) / 128) * (N / 192) >= 2L * num_cus()) tile = 9;
     else if (t128 >= 64) {
       tile = 3;
       // 128x96 when its whole-wave count x tile area beats 128x128's (5 % per-tile
@@ -955,6 +968,7 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     case 6: launch_gemm<T, 128, 256, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 7: launch_gemm<T, 128, 96, 2, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 8: launch_gemm<T, 256, 256, 2, 4, 0>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 9: launch_gemm<T, 128, 192, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     default: launch_gemm<T, 64, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
   }
 }
