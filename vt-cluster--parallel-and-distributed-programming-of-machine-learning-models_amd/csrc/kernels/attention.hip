@@ -17,8 +17,8 @@
 //            P round trip, no cross-lane shuffles for P.
 //   Tiles stream through registers: tile t+1's K/V global loads are issued
 //   before tile t's MFMAs (T14 issue-early / write-late).
-//   LDS row strides: b128-read images use HDP*2+16 B, tr-read images an odd
-//   multiple of 32 B, so both access kinds are bank-conflict free.
+//   LDS row strides: every image row is an odd multiple of 32 B, so b128 reads and
+//   transpose reads are bank-conflict free on the same image.
 // Backward (FA2 split, no atomics): attn_bwd_dq (mirror of the forward, also
 // computes D = rowsum(dO∘O) for its queries) then attn_bwd_dkdv (one key tile
 // per block, loop over query tiles; S = Q·K^T in the lane-per-key layout,
@@ -55,7 +55,12 @@ struct Geo {
   static constexpr int HDP = (HD + 31) / 32 * 32;  // padded for 32-deep K steps
   static constexpr int NKS = HDP / 32;             // K-steps over head dim
   static constexpr int NOT = HD / 16;              // 16-wide output tiles
-  static constexpr int RS = HDP * 2 + 16;          // b128-read image stride (bytes)
+  // b128-read image stride: an odd multiple of 32 B >= HDP*2, so the 8 rows a ds_read_b128 lane group
+  // (and a ds_read_b64_tr_b16 group) touches land on 8 distinct 32-B bank slots — conflict-free for
+  // BOTH access kinds (the old HDP*2+16 stride was 2-way on b128 groups and on transpose reads of
+  // the same image: 1-4 M conflicts per dispatch, profiles/r2/pmc_attention_seq.txt).  Leaves >= 32 B
+  // of padding per row (the dkdv seq kernel keeps a query's lse / D there).
+  static constexpr int RS = (((HDP * 2 + 31) / 32) | 1) * 32;
   static constexpr int TS = ((HD * 2 + 31) / 32) | 1;  // tr-read image stride / 32 (odd)
   static constexpr int TRS = TS * 32;
   static constexpr int ROW_BYTES = 64 * RS;
@@ -344,7 +349,7 @@ int attn_seq_mode() {
 }
 
 template <typename T, int HD, int NW>
-__global__ __launch_bounds__(NW * 64) void attn_fwd_seq_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+__global__ __launch_bounds__(NW * 64, 4) void attn_fwd_seq_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                               float* __restrict__ lse, const int* __restrict__ kv_len,
                                                               int B, int S, int H, float scale, uint64_t seed,
                                                               const int64_t* __restrict__ sstep, uint32_t thr,
@@ -372,6 +377,15 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_seq_kernel(const T* __restri
   const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
   const uint32_t hm0 = mift_hmix(seed, 0);
 
+  const int ng = (S + 15) / 16;
+  // Q fragments of this wave's first two 16-query groups are requested before K/V are staged, so
+  // their latency hides under the staging instead of stalling each group's first MFMA
+  vec8<T> qpre[2][G::NKS];
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int grp = (sl & 1) ? (sl + 1) * NW - 1 - wave : sl * NW + wave;
+    if (grp < ng) load_reg_frags<T, HD>(qpre[sl], Qg, ld, grp * 16 + qc, S, lane);
+  }
   // ---- stage K and V of the whole sequence: 8 chunks in flight per thread per round
   {
     constexpr int U = 4;
@@ -410,7 +424,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_seq_kernel(const T* __restri
   }
   __syncthreads();
 
-  const int ng = (S + 15) / 16;
   T* Og = out + (int64_t)b * S * D + h * HD;
   for (int slot = 0;; ++slot) {
     const int grp = (slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave;  // snake order
@@ -418,7 +431,12 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_seq_kernel(const T* __restri
     if (grp >= ng) continue;
     const int q0 = grp * 16, myq = q0 + qc;
     vec8<T> qf[G::NKS];
-    load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
+    if (slot < 2) {
+#pragma unroll
+      for (int s = 0; s < G::NKS; ++s) qf[s] = slot == 0 ? qpre[0][s] : qpre[1][s];
+    } else {
+      load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
+    }
     float m = -INFINITY, l = 0.f;
     float4_ o[G::NOT];
 #pragma unroll
@@ -811,7 +829,7 @@ MIFT_HD void stage_rows(char* img, const T* src, int64_t ld, int S, int SP, int 
 }
 
 template <typename T, int HD, int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
+__global__ __launch_bounds__(NW * 64, 4) void attn_bwd_dq_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
                                                                  const T* __restrict__ dout, const float* __restrict__ lse,
                                                                  float* __restrict__ Dv, T* __restrict__ dqkv,
                                                                  const int* __restrict__ kv_len, int B, int S, int H,
@@ -842,22 +860,22 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_seq_kernel(const T* __res
   const float c2 = scale * LOG2E;
   const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
   const uint32_t hm0 = mift_hmix(seed, 0);
+  const int ng = (S + 15) / 16;
   stage_rows<T, HD>(Ks, Kg, ld, S, SP, tid, NT);
   stage_rows<T, HD>(Vs, Vg, ld, S, SP, tid, NT);
   __syncthreads();
   T* dQg = dqkv + (int64_t)b * S * ld + h * HD;
-  const int ng = (S + 15) / 16;
   for (int slot = 0;; ++slot) {
     const int grp = (slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave;
     if (slot * NW >= ng) break;
     if (grp >= ng) continue;
     const int q0 = grp * 16, myq = q0 + qc;
     vec8<T> qf[G::NKS], df[G::NKS];
-    load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
-    load_reg_frags<T, HD>(df, dOg, D, myq, S, lane);
     float Dq = 0.f;
     {
       vec8<T> of[G::NKS];
+      load_reg_frags<T, HD>(qf, Qg, ld, myq, S, lane);
+      load_reg_frags<T, HD>(df, dOg, D, myq, S, lane);
       load_reg_frags<T, HD>(of, Og, D, myq, S, lane);
 #pragma unroll
       for (int s = 0; s < G::NKS; ++s)
@@ -920,7 +938,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_seq_kernel(const T* __res
 }
 
 template <typename T, int HD, int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+__global__ __launch_bounds__(NW * 64, 4) void attn_bwd_dkdv_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                                    const float* __restrict__ lse,
                                                                    const float* __restrict__ Dv, T* __restrict__ dqkv,
                                                                    const int* __restrict__ kv_len, int B, int S, int H,
@@ -932,10 +950,12 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_seq_kernel(const T* __r
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int SP = (S + BKV - 1) / BKV * BKV;
-  char* Qs = smem;                          // Q rows (A of S; tr-read B of dK)
-  char* dOs = smem + (size_t)SP * G::RS;    // dO rows (A of dP; tr-read B of dV)
-  float* lse_s = reinterpret_cast<float*>(dOs + (size_t)SP * G::RS);
-  float* D_s = lse_s + SP;
+  char* Qs = smem;                          // Q rows (A of S; tr-read B of dK); lse·log2e in the row padding
+  char* dOs = smem + (size_t)SP * G::RS;    // dO rows (A of dP; tr-read B of dV); D in the row padding
+  constexpr int PADOFF = G::HDP * 2;        // first padding byte of a row (RS - HDP*2 >= 32)
+  static_assert(G::RS - PADOFF >= 4, "row padding holds one float");
+  auto lse_at = [&](int q) { return *reinterpret_cast<const float*>(Qs + (size_t)q * G::RS + PADOFF); };
+  auto D_at = [&](int q) { return *reinterpret_cast<const float*>(dOs + (size_t)q * G::RS + PADOFF); };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, kc = lane & 15;
@@ -950,17 +970,17 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_seq_kernel(const T* __r
   const int klen = kv_len ? kv_len[b] : S;
   MIFT_ASSERT(klen >= 0 && klen <= S);
   const float c2 = scale * LOG2E;
+  const int ng = (S + 15) / 16;
   stage_rows<T, HD>(Qs, Qg, ld, S, SP, tid, NT);
   stage_rows<T, HD>(dOs, dOg, D, S, SP, tid, NT);
   for (int i = tid; i < SP; i += NT) {
     const int q = min(i, S - 1);
-    lse_s[i] = lse[(int64_t)bh * S + q] * LOG2E;
-    D_s[i] = Dv[(int64_t)bh * S + q];
+    *reinterpret_cast<float*>(Qs + (size_t)i * G::RS + PADOFF) = lse[(int64_t)bh * S + q] * LOG2E;
+    *reinterpret_cast<float*>(dOs + (size_t)i * G::RS + PADOFF) = Dv[(int64_t)bh * S + q];
   }
   __syncthreads();
   T* dKg = dqkv + (int64_t)b * S * ld + D + h * HD;
   T* dVg = dKg + D;
-  const int ng = (S + 15) / 16;
   const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
   const uint32_t hm0 = mift_hmix(seed, 0);
   for (int slot = 0;; ++slot) {
@@ -1014,7 +1034,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_seq_kernel(const T* __r
         for (int r = 0; r < 4; ++r) {
           const int ql = qb + t * 16 + g * 4 + r;
           bool valid = true;
-          float pr = fast_exp2(sa[r] * c2 - lse_s[ql]);
+          float pr = fast_exp2(sa[r] * c2 - lse_at(ql));
           if (!interior) {
             valid = ql < S && mykey <= ql && mykey < klen;
             if (!valid) pr = 0.f;
@@ -1028,7 +1048,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_seq_kernel(const T* __r
             dp = kp ? dp * inv_keep : 0.f;
           }
           pf[t >> 1][(t & 1) * 4 + r] = (T)pd;
-          dsf[t >> 1][(t & 1) * 4 + r] = (T)(pr * (dp - D_s[ql]));
+          dsf[t >> 1][(t & 1) * 4 + r] = (T)(pr * (dp - D_at(ql)));
         }
       }
 #pragma unroll
@@ -1098,7 +1118,7 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
   using G = Geo<HD>;
   const int seq_env = attn_seq_mode();
   const int SP = (S + BKV - 1) / BKV * BKV;
-  const int seq_dq = 2 * SP * G::RS, seq_kv = 2 * SP * G::RS + 2 * SP * 4;
+  const int seq_dq = 2 * SP * G::RS, seq_kv = 2 * SP * G::RS;  // dkdv: lse / D live in the row padding
   if (seq_env && 2 * seq_kv <= 160 * 1024 && (B * H >= 256 || seq_env == 2)) {  // whole sequence in LDS, 2 blocks per CU
     auto kq = attn_bwd_dq_seq_kernel<T, HD, 8>;
     auto kk = attn_bwd_dkdv_seq_kernel<T, HD, 8>;
