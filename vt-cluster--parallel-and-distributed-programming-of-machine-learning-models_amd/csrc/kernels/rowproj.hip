@@ -196,185 +196,6 @@ __global__ __launch_bounds__(256) void mask_proj_kernel(const T* __restrict__ x,
   reduce_store<T, LR>(acc, pout + (size_t)row * 32, lane, alpha);
 }
 
-// ---- multi-row variants (rank <= 8): each wave keeps its [8, D] slice of pw (packed 16-bit) and,
-// for ln_fwd_proj, the LN weight/bias in registers and walks RPW rows, prefetching row r+1 while
-// row r is reduced.  The one-row kernels above re-read pw (12 KiB at D = 768) from L1/L2 for every
-// row — 4x the row's own bytes — and ran at 1.6 TB/s of essential traffic (mask_proj 16 us, ln_fwd_proj
-// 19 us per 8192 x 768 call in the distilgpt2 step).
-template <int NIT>
-struct RowRegs {
-  short4_ v[NIT];
-};
-
-template <typename T, int NIT>
-MIFT_HD void load_row(RowRegs<NIT>& r, const T* xr, int D, int lane) {
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int c = (it * 64 + lane) * VEC;
-    r.v[it] = c < D ? *reinterpret_cast<const short4_*>(xr + c) : short4_{0, 0, 0, 0};
-  }
-}
-
-template <typename T>
-MIFT_HD void unpack4(short4_ v, float* o) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { short s = v[i]; T t; __builtin_memcpy(&t, &s, 2); o[i] = (float)t; }
-}
-
-template <typename T, int NIT, int RPW>
-__global__ __launch_bounds__(256) void mask_proj_rows_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                             const T* __restrict__ pw, T* __restrict__ pout, int M,
-                                                             int D, float alpha, uint64_t seed,
-                                                             const int64_t* __restrict__ sstep, uint32_t thr,
-                                                             float inv_keep) {
-  constexpr int LR = 8;
-  seed = mift_seed(seed, sstep);
-  const int lane = threadIdx.x & 63;
-  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-  if (row0 >= M) return;
-  short4_ wr[NIT][LR];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int c = (it * 64 + lane) * VEC;
-#pragma unroll
-    for (int j = 0; j < LR; ++j)
-      wr[it][j] = c < D ? *reinterpret_cast<const short4_*>(pw + (size_t)j * D + c) : short4_{0, 0, 0, 0};
-  }
-  RowRegs<NIT> cur, nxt;
-  load_row<T, NIT>(cur, x + (size_t)row0 * D, D, lane);
-#pragma unroll 1
-  for (int rr = 0; rr < RPW; ++rr) {
-    const int row = row0 + rr;
-    if (row >= M) break;
-    if (rr + 1 < RPW && row + 1 < M) load_row<T, NIT>(nxt, x + (size_t)(row + 1) * D, D, lane);
-    T* yr = y + (size_t)row * D;
-    float acc[LR];
-#pragma unroll
-    for (int j = 0; j < LR; ++j) acc[j] = 0.f;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int c = (it * 64 + lane) * VEC;
-      if (c < D) {
-        float v[VEC];
-        unpack4<T>(cur.v[it], v);
-        if (thr != 0) {
-          bool kp[VEC];
-          mift_keep4(seed, (uint64_t)row * D + c, thr, kp);
-#pragma unroll
-          for (int i = 0; i < VEC; ++i) v[i] = kp[i] ? v[i] * inv_keep : 0.f;
-          st4<T>(yr + c, v);
-        }
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) v[i] = rnd<T>(v[i]);
-#pragma unroll
-        for (int j = 0; j < LR; ++j) {
-          float a[VEC];
-          unpack4<T>(wr[it][j], a);
-#pragma unroll
-          for (int i = 0; i < VEC; ++i) acc[j] += v[i] * a[i];
-        }
-      }
-    }
-    reduce_store<T, LR>(acc, pout + (size_t)row * 32, lane, alpha);
-    cur = nxt;
-  }
-}
-
-template <typename T, typename W, int NIT, int RPW>
-__global__ __launch_bounds__(256) void ln_fwd_proj_rows_kernel(const T* __restrict__ x, const W* __restrict__ w,
-                                                               const W* __restrict__ b, T* __restrict__ y,
-                                                               float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                               const T* __restrict__ pw, T* __restrict__ pout, int M,
-                                                               int D, float eps, float alpha, uint64_t seed,
-                                                               const int64_t* __restrict__ sstep, uint32_t thr,
-                                                               float inv_keep) {
-  constexpr int LR = 8;
-  seed = mift_seed(seed, sstep);
-  const int lane = threadIdx.x & 63;
-  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-  if (row0 >= M) return;
-  short4_ wr[NIT][LR];
-  float lw[NIT][VEC], lb[NIT][VEC];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int c = (it * 64 + lane) * VEC;
-#pragma unroll
-    for (int j = 0; j < LR; ++j)
-      wr[it][j] = c < D ? *reinterpret_cast<const short4_*>(pw + (size_t)j * D + c) : short4_{0, 0, 0, 0};
-    if (c < D) {
-      ldw4<W>(w + c, lw[it]);
-      ldw4<W>(b + c, lb[it]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) lw[it][i] = lb[it][i] = 0.f;
-    }
-  }
-  RowRegs<NIT> cur, nxt;
-  load_row<T, NIT>(cur, x + (size_t)row0 * D, D, lane);
-#pragma unroll 1
-  for (int rr = 0; rr < RPW; ++rr) {
-    const int row = row0 + rr;
-    if (row >= M) break;
-    if (rr + 1 < RPW && row + 1 < M) load_row<T, NIT>(nxt, x + (size_t)(row + 1) * D, D, lane);
-    float v[NIT][VEC];
-    float s = 0.f;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      unpack4<T>(cur.v[it], v[it]);
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) s += v[it][i];
-    }
-    const float mean = wave_sum(s) / D;
-    float q = 0.f;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int c = (it * 64 + lane) * VEC;
-      if (c < D) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) { const float d = v[it][i] - mean; q += d * d; }
-      }
-    }
-    const float rstd = rsqrtf(wave_sum(q) / D + eps);
-    T* yr = y + (size_t)row * D;
-    float acc[LR];
-#pragma unroll
-    for (int j = 0; j < LR; ++j) acc[j] = 0.f;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int c = (it * 64 + lane) * VEC;
-      if (c < D) {
-        float o[VEC];
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) o[i] = (v[it][i] - mean) * rstd * lw[it][i] + lb[it][i];
-        st4<T>(yr + c, o);
-        bool kp[VEC] = {true, true, true, true};
-        if (thr != 0) mift_keep4(seed, (uint64_t)row * D + c, thr, kp);
-        float dv[VEC];
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          const float yb = rnd<T>(o[i]);
-          dv[i] = thr != 0 ? (kp[i] ? rnd<T>(yb * inv_keep) : 0.f) : yb;
-        }
-#pragma unroll
-        for (int j = 0; j < LR; ++j) {
-          float a[VEC];
-          unpack4<T>(wr[it][j], a);
-#pragma unroll
-          for (int i = 0; i < VEC; ++i) acc[j] += dv[i] * a[i];
-        }
-      }
-    }
-    if (lane == 0) {
-      mean_out[row] = mean;
-      rstd_out[row] = rstd;
-    }
-    reduce_store<T, LR>(acc, pout + (size_t)row * 32, lane, alpha);
-    cur = nxt;
-  }
-}
-
-constexpr int ROWS_PER_WAVE = 4;
-
 template <int LR, typename F>
 void by_nit(int D, F&& f) {
   const int nit = (D + 255) / 256;
@@ -431,20 +252,6 @@ std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::
       constexpr int LR = decltype(lr)::value;
       by_nit<LR>(D, [&](auto nit) {
         constexpr int NIT = decltype(nit)::value;
-        if constexpr (LR == 8 && NIT <= 4) {
-          const int grid = (M + 4 * ROWS_PER_WAVE - 1) / (4 * ROWS_PER_WAVE);
-          if (wf32)
-            ln_fwd_proj_rows_kernel<T, float, NIT, ROWS_PER_WAVE><<<grid, 256, 0, st>>>(
-                (const T*)x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), (T*)y.data_ptr(),
-                mean.data_ptr<float>(), rstd.data_ptr<float>(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, D,
-                (float)eps, (float)alpha, (uint64_t)seed, mift_seed_step(), thr, inv);
-          else
-            ln_fwd_proj_rows_kernel<T, T, NIT, ROWS_PER_WAVE><<<grid, 256, 0, st>>>(
-                (const T*)x.data_ptr(), (const T*)w.data_ptr(), (const T*)b.data_ptr(), (T*)y.data_ptr(),
-                mean.data_ptr<float>(), rstd.data_ptr<float>(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, D,
-                (float)eps, (float)alpha, (uint64_t)seed, mift_seed_step(), thr, inv);
-          return;
-        }
         if (wf32)
           ln_fwd_proj_kernel<T, float, NIT, LR><<<(M + 3) / 4, 256, 0, st>>>(
               (const T*)x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), (T*)y.data_ptr(),
@@ -484,13 +291,6 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
       constexpr int LR = decltype(lr)::value;
       by_nit<LR>(D, [&](auto nit) {
         constexpr int NIT = decltype(nit)::value;
-        if constexpr (LR == 8 && NIT <= 4) {
-          const int grid = (M + 4 * ROWS_PER_WAVE - 1) / (4 * ROWS_PER_WAVE);
-          mask_proj_rows_kernel<T, NIT, ROWS_PER_WAVE><<<grid, 256, 0, st>>>(
-              (const T*)x.data_ptr(), (T*)y.data_ptr(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, D,
-              (float)alpha, (uint64_t)seed, mift_seed_step(), thr, inv);
-          return;
-        }
         mask_proj_kernel<T, NIT, LR><<<(M + 3) / 4, 256, 0, st>>>((const T*)x.data_ptr(), (T*)y.data_ptr(),
                                                                   (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, D,
                                                                   (float)alpha, (uint64_t)seed, mift_seed_step(), thr, inv);
