@@ -28,16 +28,6 @@ for r in range(R):
     row["torch"] = round(t(lambda: torch.matmul(a, w.t())), 1)
     print(row, flush=True)
 
-# persistent fused head A/B (MIFT_LM_PERSIST = blocks per CU, 0 = one block per tile)
-os.environ["MIFT_LM_DBG"] = "0"
-for r in range(R):
-    row = {}
-    for pz in ("0", "1", "2"):
-        os.environ["MIFT_LM_PERSIST"] = pz
-        row["persist" + pz] = round(t(lambda: C.lmhead_fwd(a, w, lab, V, 0)), 1)
-    os.environ.pop("MIFT_LM_PERSIST")
-    print(row, flush=True)
-
 # tile raster A/B (MIFT_GEMM_GROUP, read per call) on the fused head and OPT-scale plain GEMMs
 os.environ["MIFT_LM_DBG"] = "0"
 shapes = [("lm_head", a, w)]

@@ -349,7 +349,7 @@ int attn_seq_mode() {
 }
 
 template <typename T, int HD, int NW>
-__global__ __launch_bounds__(NW * 64, 4) void attn_fwd_seq_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+__global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                               float* __restrict__ lse, const int* __restrict__ kv_len,
                                                               int B, int S, int H, float scale, uint64_t seed,
                                                               const int64_t* __restrict__ sstep, uint32_t thr,
@@ -829,7 +829,7 @@ MIFT_HD void stage_rows(char* img, const T* src, int64_t ld, int S, int SP, int 
 }
 
 template <typename T, int HD, int NW>
-__global__ __launch_bounds__(NW * 64, 4) void attn_bwd_dq_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
+__global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
                                                                  const T* __restrict__ dout, const float* __restrict__ lse,
                                                                  float* __restrict__ Dv, T* __restrict__ dqkv,
                                                                  const int* __restrict__ kv_len, int B, int S, int H,
@@ -938,7 +938,7 @@ __global__ __launch_bounds__(NW * 64, 4) void attn_bwd_dq_seq_kernel(const T* __
 }
 
 template <typename T, int HD, int NW>
-__global__ __launch_bounds__(NW * 64, 4) void attn_bwd_dkdv_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+__global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                                    const float* __restrict__ lse,
                                                                    const float* __restrict__ Dv, T* __restrict__ dqkv,
                                                                    const int* __restrict__ kv_len, int B, int S, int H,

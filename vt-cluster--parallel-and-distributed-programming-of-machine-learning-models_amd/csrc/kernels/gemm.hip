@@ -582,9 +582,13 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     const int V = lm.V;
     constexpr float L2E = 1.4426950408889634f;
     // labels first: their load latency hides under the max pass (they are consumed after a barrier)
-    int64_t labs[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) labs[i] = lm_label(lm.labels, min(m0 + wm * WM + i * 16 + fr, M - 1), lm.shift);
+    // the block's row targets go to LDS (read after the max-pass barrier): requested first so their
+    // latency hides under the max pass, and no registers held across it (the kernel sits at 256)
+    int* labs = reinterpret_cast<int*>(reds + NW * WM);
+    if (tid < BM) {
+      const int64_t l = lm_label(lm.labels, min(m0 + tid, M - 1), lm.shift);
+      labs[tid] = (l >= 0 && l < V) ? (int)l : -1;
+    }
     const bool full = n0 + BN <= V;  // block-uniform: only the last column tile holds padding columns
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -608,7 +612,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       if (m == -INFINITY) m = 0.f;  // tile entirely beyond V (cannot happen for V_pad - V < BN)
       const int lrow = wm * WM + i * 16 + fr;
       const int row = m0 + lrow;
-      const int64_t lab = row < M ? labs[i] : -1;
+      const int lab = row < M ? labs[lrow] : -1;
       const float mb = m * L2E;
       float s = 0.f;
 #pragma unroll
@@ -622,8 +626,8 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
                   : (full || col + e < V) ? __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][e], L2E, -mb)) : 0.f;
           s += ev[e];
         }
-        const int64_t d = lab - col;
-        if (d >= 0 && d < 4 && lab < V) {  // static selects: a runtime vector index would go to scratch
+        const int d = lab - col;
+        if (d >= 0 && d < 4) {  // static selects: a runtime vector index would go to scratch
           const float4_ a = acc[i][j];
           lm.zlab[row] = d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
         }
@@ -662,11 +666,12 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   const int nk_all = K / BK;
   if constexpr (EPI == 1) {
     static_assert(NSTAGE == 0, "LM-head forward runs on the phased 256x256 tile");
-    // persistent when gridDim.x < tiles (MIFT_LM_PERSIST): block b walks tiles b, b + grid, ...,
-    // all on its own XCD (grid % 8 == 0), so the E stores of one tile drain while the next tile's
-    // main loop runs instead of holding the CU until the block retires
+    // one block per tile: a persistent loop over tiles (E stores draining under the next tile's main
+    // loop) measured 2-3 % faster in isolation but pushed the kernel past 256 VGPRs into scratch
+    // spills; with the row targets in LDS the one-tile kernel needs 220 and no spills
     const int nblk = ntm * ntn;
-    for (int t0 = blockIdx.x; t0 < nblk; t0 += gridDim.x) {
+    {
+      const int t0 = blockIdx.x;
       int bid = t0;
       {
         const int q = nblk / 8, r = nblk % 8;
@@ -685,7 +690,6 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
       mainloop8(0, nk_all, [](int) {});
       lm_fwd_epilogue();
-      __syncthreads();  // the E tile in LDS is read out before the next prologue restages the ring
     }
     return;
   } else if constexpr (EPI == 2) {
@@ -1058,7 +1062,7 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   }
   SkArgs sk{};
   // staging ring (128 KiB) reused for the E tile + the two row-partial arrays
-  constexpr int SMEM = std::max(2 * (BM + BN) * ROWB, BM * (BN + 8) * 2 + 2 * 8 * (BM / 2) * 4);
+  constexpr int SMEM = std::max(2 * (BM + BN) * ROWB, BM * (BN + 8) * 2 + 2 * 8 * (BM / 2) * 4 + BM * 4);
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>;
   static bool attr = false;
@@ -1067,14 +1071,7 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
     attr = true;
   }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-  int grid = ntm * ntn;
-  {
-    // blocks per CU of the persistent grid (0 = one block per tile): one per CU measured 3-6 % faster
-    // than one block per tile (tools/diag_lmhead.py: 772 vs 793 us, 788 vs 836 us on two boxes)
-    const char* pe = getenv("MIFT_LM_PERSIST");
-    const int per = pe ? atoi(pe) : 1;
-    if (per > 0) grid = std::min(grid, per * num_cus());
-  }
+  const int grid = ntm * ntn;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
                      (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
   hipLaunchKernelGGL(lmhead_lse_kernel, dim3((M + 3) / 4), dim3(256), 0, st,
