@@ -62,6 +62,9 @@ def build_argparser(defaults=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--step_log", choices=["p1", "lab", "none"], default="p1")
     ap.add_argument("--no_save", action="store_true")
+    ap.add_argument("--profile", type=str, default=None,
+                    help="dir: torch.profiler trace + kernel table + named-range ms per rank (mift.obs.profiler)")
+    ap.add_argument("--profile_steps", type=str, default="3:6", help="global optimizer steps A:B (B exclusive)")
     ap.add_argument("--run_name", type=str, default=None, help="fixed run dir name (resume across jobs)")
     ap.add_argument("--config", type=str, default=None,
                     help="run config JSON (DeepSpeed keys + mift.* keys, mift.config.MiftConfig)")
@@ -147,7 +150,7 @@ def main(argv=None, defaults=None):
                        recompute=bool(args.gradient_checkpointing) or mcfg.activation_checkpointing,
                        step_log=args.step_log, seed=args.seed, bucket_mb=mcfg.bucket_mb, graph=mcfg.graph,
                        consistency_every=mcfg.consistency_every, max_grad_norm=mcfg.gradient_clipping,
-                       weight_decay=mcfg.weight_decay)
+                       weight_decay=mcfg.weight_decay, profile_dir=args.profile, profile_steps=args.profile_steps)
     trainer = Trainer(model, batcher, tcfg, ctx)
     logs.log("Trainer setup", time.perf_counter() - t0)
 

@@ -72,6 +72,9 @@ def build_argparser():
     ap.add_argument("--lora_dropout", type=float, default=0.05)
     ap.add_argument("--target_modules", default="q_proj,k_proj,v_proj,out_proj,fc1,fc2")
     ap.add_argument("--max_steps", type=int, default=-1)
+    ap.add_argument("--profile", type=str, default=None,
+                    help="dir: torch.profiler trace + kernel table + named-range ms per rank (mift.obs.profiler)")
+    ap.add_argument("--profile_steps", type=str, default="3:6", help="global optimizer steps A:B (B exclusive)")
     ap.add_argument("--log_every", type=int, default=10)
     ap.add_argument("--gradient_checkpointing", type=int, default=0)
     ap.add_argument("--seed", type=int, default=0)
@@ -171,7 +174,7 @@ def main(argv=None):
                        bucket_mb=ds.bucket_mb, graph=ds.graph, consistency_every=ds.consistency_every,
                        save_steps=args.save_steps,
                        output_dir=os.path.join(args.out_root, "checkpoints") if args.save_steps else None,
-                       resume=args.resume)
+                       resume=args.resume, profile_dir=args.profile, profile_steps=args.profile_steps)
     t_last = [time.perf_counter()]
 
     def p2_log(trainer, rec):

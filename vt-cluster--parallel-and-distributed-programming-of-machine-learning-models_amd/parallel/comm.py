@@ -16,6 +16,8 @@ Reference parity: DeepSpeed's pipeline p2p (``deepspeed.runtime.pipe.p2p``,
 import torch
 import torch.distributed as dist
 
+from ..obs.profiler import rng
+
 
 def backend_of(group=None):
     return dist.get_backend(group) if dist.is_initialized() else "none"
@@ -73,7 +75,8 @@ class P2P:
                 copies.append((t, dst))
             keep.append(dst)
             ops.append(dist.P2POp(dist.irecv, dst, peer, group=self.group))
-        works = dist.batch_isend_irecv(ops)
+        with rng(f"mift.pp.p2p.s{len(sends)}r{len(recvs)}"):
+            works = dist.batch_isend_irecv(ops)
         return Pending(works, [t for t, _ in recvs], copies, keep)
 
     def exchange(self, sends=(), recvs=()):

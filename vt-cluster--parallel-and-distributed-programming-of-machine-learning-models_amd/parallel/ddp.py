@@ -24,6 +24,8 @@ import contextlib
 import torch
 import torch.distributed as dist
 
+from ..obs.profiler import rng
+
 
 class GradReducer:
     def __init__(self, arena, group=None, bucket_mb: float = 25.0, overlap: bool = True, world: int = None):
@@ -78,7 +80,8 @@ class GradReducer:
             from ..ops.streams import join
             join()  # wgrad kernels queued on the side stream are ordered before the collective
         sl = self.arena.grad[b["lo"]:b["hi"]]
-        self.handles.append(dist.all_reduce(sl, group=self.group, async_op=True))
+        with rng(f"mift.comm.bucket{b['idx']}.{where}"):
+            self.handles.append(dist.all_reduce(sl, group=self.group, async_op=True))
         b["launched"] = True
         self.launch_log.append((b["idx"], where))
 

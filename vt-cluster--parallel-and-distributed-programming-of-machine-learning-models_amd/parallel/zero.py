@@ -17,6 +17,7 @@ adapters; reduce-scatter + all-gather move the same bytes as one all-reduce.
 """
 import torch
 
+from ..obs.profiler import rng
 from ..train.optim import FusedAdamW
 from .comm import all_gather_flat, reduce_scatter_flat
 
@@ -46,12 +47,14 @@ class Zero1AdamW:
         self.opt.set_lr(lr)
 
     def reduce_grads(self):
-        reduce_scatter_flat(self.gshard, self.arena.grad, self.group)
+        with rng("mift.comm.zero_rs"):
+            reduce_scatter_flat(self.gshard, self.arena.grad, self.group)
         self.arena.grad.zero_()
 
     def step(self):
         self.opt.step()
-        all_gather_flat(self.arena.param, self.arena.param[self.lo:self.hi].clone(), self.group)
+        with rng("mift.comm.zero_ag"):
+            all_gather_flat(self.arena.param, self.arena.param[self.lo:self.hi].clone(), self.group)
 
     def stats(self):
         return self.opt.stats()

@@ -29,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from ..lora import LoraArena, adapter_state_dict, save_adapter
+from ..obs.profiler import StepProfiler, parse_window, rng
 from ..obs.timing import HOST, hf_log_line, lab_step_line, p1_step_line, perf_line
 from ..parallel.ddp import GradReducer, verify_replicas
 from ..utils.faults import maybe_inject
@@ -61,6 +62,8 @@ class TrainConfig:
     logging_first_step: bool = False
     graph: str = "auto"                # hipGraph-replayed steps (mift.train.graph): auto | on | off (MIFT_GRAPH)
     consistency_every: int = 0         # >0: checksum the trainable params across DP replicas every N steps
+    profile_dir: Optional[str] = None  # torch.profiler window (mift.obs.profiler): trace/kernels/ranges per rank
+    profile_steps: str = "3:6"         # global steps [A, B) recorded when profile_dir is set
 
 
 class Trainer:
@@ -176,6 +179,10 @@ class Trainer:
 
     def train_step(self, mbs):
         """One optimizer step over a list of micro-batches. Returns loss_sum tensor."""
+        with rng("mift.step"):
+            return self._train_step(mbs)
+
+    def _train_step(self, mbs):
         model, cfg = self.model, self.cfg
         ntok = self._global_tokens(mbs)
         if self.reducer is not None:
@@ -183,12 +190,15 @@ class Trainer:
         lr = self.sched(self.global_step)
         self.opt.set_lr(lr)
         if self.graphed is not None and self.graphed.supported(mbs):
-            return self._finish_step(self.graphed.run(mbs, ntok), ntok)
+            with rng("mift.fwd_bwd.graph"):
+                loss = self.graphed.run(mbs, ntok)
+            return self._finish_step(loss, ntok)
         gscale = self.opt.loss_scale_t / ntok
         if self.engine is not None:
             dev_mbs = [self._to_dev(mb) for mb in mbs]
             ms0 = model.micro_step
-            loss_acc = self.engine.train_batch(dev_mbs, gscale, ms0 + 1)
+            with rng("mift.fwd_bwd.pipeline"):
+                loss_acc = self.engine.train_batch(dev_mbs, gscale, ms0 + 1)
             model.micro_step = ms0 + len(mbs)
             maybe_inject(self.rank, self.global_step + 1, "micro")
             return self._finish_step(loss_acc, ntok)
@@ -199,7 +209,7 @@ class Trainer:
             model.next_micro_step()
             last = i == len(mbs) - 1
             ctxm = self.reducer.no_sync() if (not last and self.reducer is not None) else _null()
-            with ctxm:
+            with ctxm, rng("mift.fwd_bwd"):
                 with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
                     out = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"],
                                 labels=mb["labels"], reduction="sum", return_logits=False)
@@ -219,13 +229,15 @@ class Trainer:
             if self._comm_ev is None:
                 self._comm_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self._comm_ev[0].record()
-        if self.zero:
-            self.opt.reduce_grads()
-        else:
-            self.reducer.finish()
+        with rng("mift.comm.grads"):
+            if self.zero:
+                self.opt.reduce_grads()
+            else:
+                self.reducer.finish()
         if timed:
             self._comm_ev[1].record()
-        self.opt.step()
+        with rng("mift.optimizer"):
+            self.opt.step()
         self.arena.bump()
         self.global_step += 1
         return loss_acc, ntok
@@ -251,10 +263,16 @@ class Trainer:
         sync_dev = self.device.type == "cuda"
         epoch = start_step // max(1, self.steps_per_epoch)
         done = start_step >= self.total_steps
+        prof = (StepProfiler(cfg.profile_dir, self.rank, parse_window(cfg.profile_steps))
+                if cfg.profile_dir else None)
         while not done:
             skip = start_step - epoch * self.steps_per_epoch
             for mbs in self.batcher.epoch(epoch, start_step=max(0, skip)):
+                if prof is not None:
+                    prof.before_step(self.global_step + 1)
                 loss_sum, ntok = self.train_step(mbs)
+                if prof is not None:
+                    prof.after_step(self.global_step)
                 maybe_inject(self.rank, self.global_step, "step")
                 log_now = bool(cfg.logging_steps) and (self.global_step % cfg.logging_steps == 0 or
                                                        (cfg.logging_first_step and self.global_step == 1))
@@ -296,6 +314,8 @@ class Trainer:
             start_step = epoch * self.steps_per_epoch
             if epoch * self.steps_per_epoch >= self.total_steps:
                 done = True
+        if prof is not None:
+            prof.close()  # window longer than the run: dump what was recorded
         if sync_dev:
             torch.cuda.synchronize()
         return self.history
