@@ -202,6 +202,30 @@ def test_flash_attention_whole_sequence_kernels(S, p, dt, monkeypatch):
     torch.testing.assert_close(d_seq.float(), d_til.float(), atol=2e-3, rtol=2e-3)
 
 
+@pytest.mark.parametrize("hd,S", [(64, 256), (64, 200), (32, 384), (80, 128), (128, 100)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_attention_keep_bits_match_hash(hd, S, dt, monkeypatch):
+    """Dropout keep bits recorded by the whole-sequence forward (attn_fwd_bits) and read by the
+    backward give exactly the re-hashing backward: same masks, same arithmetic -> equal dqkv."""
+    monkeypatch.setenv("MIFT_ATTN_SEQ", "2")
+    C = _C()
+    torch.manual_seed(11)
+    B, H, p = 2, 3, 0.1
+    qkv = torch.randn(B * S, 3 * H * hd, device="cuda").to(dt)
+    kvl = torch.tensor([S - 9, S // 3], device="cuda", dtype=torch.int32)
+    for lens in (None, kvl):
+        o, lse = C.attn_fwd(qkv, B, S, H, hd, hd ** -0.5, p, 77, lens)
+        o2, lse2, bits = C.attn_fwd_bits(qkv, B, S, H, hd, hd ** -0.5, p, 77, lens)
+        torch.testing.assert_close(o2, o, atol=0, rtol=0)
+        torch.testing.assert_close(lse2, lse, atol=0, rtol=0)
+        do = torch.randn_like(o)
+        d_hash = C.attn_bwd(do, qkv, o, lse, B, S, H, hd, hd ** -0.5, p, 77, lens)
+        d_bits = C.attn_bwd_bits(do, qkv, o, lse, B, S, H, hd, hd ** -0.5, p, 77, lens, bits if bits.numel() else None)
+        torch.testing.assert_close(d_bits, d_hash, atol=0, rtol=0)
+        if hd == 64:
+            assert bits.numel() == B * H * S * ((S + 63) // 64 * 4)  # the record exists on this path
+
+
 def test_flash_attention_kv_len():
     C = _C()
     torch.manual_seed(7)

@@ -353,12 +353,13 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
                                                               float* __restrict__ lse, const int* __restrict__ kv_len,
                                                               int B, int S, int H, float scale, uint64_t seed,
                                                               const int64_t* __restrict__ sstep, uint32_t thr,
-                                                              float inv_keep) {
+                                                              float inv_keep, uint16_t* __restrict__ dmask) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int SP = (S + BKV - 1) / BKV * BKV;  // image rows (zero padded to whole key tiles)
+  const int NR = SP / 16;                    // keep-bit record: uint16 elements per query (see KEEP BITS)
   char* Ks = smem;                           // [SP][RS] b128 image
   char* Vs = smem + (size_t)SP * G::RS;      // [SP][TRS] tr image
   const int tid = threadIdx.x, lane = tid & 63;
@@ -478,6 +479,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
       }
       vec8<T> pf[2];
       float psum = 0.f;
+      uint32_t kbits[2] = {0u, 0u};  // this lane's keep nibbles, placed at their record bits
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bool kp[4] = {true, true, true, true};
@@ -485,6 +487,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
           const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
           if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
           else mift_keep4(seed, i0, thr, kp);
+          const uint32_t nib = (uint32_t)kp[0] | ((uint32_t)kp[1] << 1) | ((uint32_t)kp[2] << 2) | ((uint32_t)kp[3] << 3);
+          kbits[t >> 1] |= nib << ((t & 1) * 16 + g * 4);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -493,6 +497,17 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
           if (thr != 0) pv = kp[r] ? pv * inv_keep : 0.f;
           pf[t >> 1][(t & 1) * 4 + r] = (T)pv;
         }
+      }
+      if (dmask != nullptr) {
+        // KEEP BITS: record element kt*4 + t of query myq holds keys k0 + 16t + 0..15 (bit j <-> key
+        // k0 + 16t + j); the four g-lanes of a query each own one nibble of every element
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          kbits[h2] |= __shfl_xor(kbits[h2], 16, 64);
+          kbits[h2] |= __shfl_xor(kbits[h2], 32, 64);
+        }
+        if (g == 0 && myq < S)
+          *reinterpret_cast<uint2*>(dmask + ((int64_t)bh * S + myq) * NR + kt * 4) = make_uint2(kbits[0], kbits[1]);
       }
       l = l * alpha + psum;
       if (resc) {
@@ -835,12 +850,14 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
                                                                  const int* __restrict__ kv_len, int B, int S, int H,
                                                                  float scale, uint64_t seed,
                                                                  const int64_t* __restrict__ sstep, uint32_t thr,
-                                                                 float inv_keep) {
+                                                                 float inv_keep, const uint16_t* __restrict__ dmask) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int SP = (S + BKV - 1) / BKV * BKV;
+  constexpr int PADOFF = G::HDP * 2;      // row padding [PADOFF, RS) = 32 B per row of each image
+  static_assert(G::RS - PADOFF == 32, "32-B row padding");
   char* Ks = smem;                        // K rows (A of S^T; tr-read B of dQ)
   char* Vs = smem + (size_t)SP * G::RS;   // V rows (A of dP^T)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -863,6 +880,18 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
   const int ng = (S + 15) / 16;
   stage_rows<T, HD>(Ks, Kg, ld, S, SP, tid, NT);
   stage_rows<T, HD>(Vs, Vg, ld, S, SP, tid, NT);
+  // keep-bit records of the forward (KEEP BITS): query q's record goes to the row-q padding, 8-B
+  // words 0..3 (64-key tiles 0..3) in the K image, 4..7 in the V image
+  const int NW4 = SP / 64;
+  const bool mk = dmask != nullptr;
+  if (mk) {
+    MIFT_ASSERT(NW4 <= 8);
+    for (int i = tid; i < S * NW4; i += NT) {
+      const int q = i / NW4, w = i % NW4;
+      const uint2 v = *reinterpret_cast<const uint2*>(dmask + ((int64_t)bh * S + q) * (NW4 * 4) + w * 4);
+      *reinterpret_cast<uint2*>((w < 4 ? Ks : Vs) + (size_t)q * G::RS + PADOFF + (w & 3) * 8) = v;
+    }
+  }
   __syncthreads();
   T* dQg = dqkv + (int64_t)b * S * ld + h * HD;
   for (int slot = 0;; ++slot) {
@@ -895,6 +924,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
       const int k0 = kt * BKV;
       vec8<T> dsf[2];
       const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
+      uint2 kw = make_uint2(0u, 0u);
+      if (mk) kw = *reinterpret_cast<const uint2*>((kt < 4 ? Ks : Vs) + (size_t)min(myq, S - 1) * G::RS + PADOFF + (kt & 3) * 8);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         float4_ sa = float4_{0.f, 0.f, 0.f, 0.f}, pa = float4_{0.f, 0.f, 0.f, 0.f};
@@ -904,7 +935,11 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
           pa = mfma16(ld_frag<T>(Vs + (k0 + t * 16 + qc) * G::RS + (4 * s + g) * 16), df[s], pa);
         }
         bool kp[4] = {true, true, true, true};
-        if (thr != 0) {
+        if (mk) {
+          const uint32_t e = ((t < 2 ? kw.x : kw.y) >> ((t & 1) * 16 + g * 4)) & 0xFu;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) kp[r] = (e >> r) & 1u;
+        } else if (thr != 0) {
           const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
           if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
           else mift_keep4(seed, i0, thr, kp);
@@ -944,7 +979,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
                                                                    const int* __restrict__ kv_len, int B, int S, int H,
                                                                    float scale, uint64_t seed,
                                                                    const int64_t* __restrict__ sstep, uint32_t thr,
-                                                                   float inv_keep) {
+                                                                   float inv_keep, const uint16_t* __restrict__ dmask) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   constexpr int NT = NW * 64;
@@ -977,6 +1012,23 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
     const int q = min(i, S - 1);
     *reinterpret_cast<float*>(Qs + (size_t)i * G::RS + PADOFF) = lse[(int64_t)bh * S + q] * LOG2E;
     *reinterpret_cast<float*>(dOs + (size_t)i * G::RS + PADOFF) = Dv[(int64_t)bh * S + q];
+  }
+  // keep-bit records of the forward (KEEP BITS), element e of query q after the lse (e < 14) or the
+  // D (e >= 14) float of row q: 28 B of padding per image row
+  const int NR = SP / 16;
+  const bool mk = dmask != nullptr;
+  auto rec_at = [&](int q, int e) -> char* {
+    return (e < 14 ? Qs + (size_t)q * G::RS + PADOFF + 4 + e * 2 : dOs + (size_t)q * G::RS + PADOFF + 4 + (e - 14) * 2);
+  };
+  if (mk) {
+    MIFT_ASSERT(NR <= 28);
+    for (int i = tid; i < S * (NR / 4); i += NT) {
+      const int q = i / (NR / 4), w = i % (NR / 4);
+      const uint2 v = *reinterpret_cast<const uint2*>(dmask + ((int64_t)bh * S + q) * NR + w * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<uint16_t*>(rec_at(q, w * 4 + j)) = (uint16_t)(((j < 2 ? v.x : v.y) >> ((j & 1) * 16)) & 0xFFFFu);
+    }
   }
   __syncthreads();
   T* dKg = dqkv + (int64_t)b * S * ld + D + h * HD;
@@ -1011,7 +1063,12 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
           pa = mfma16(ld_frag<T>(dOs + (qb + t * 16 + kc) * G::RS + (4 * s + g) * 16), vf[s], pa);
         }
         uint32_t hb[4] = {0, 0, 0, 0};
-        if (thr != 0) {
+        if (mk) {
+          // keep bit of (query, mykey): element grp = k0 / 16 of the query's record, bit kc
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            hb[r] = *reinterpret_cast<const uint16_t*>(rec_at(min(qb + t * 16 + g * 4 + r, S - 1), grp));
+        } else if (thr != 0) {
           const int odd = kc & 1;
           const int qa = min(qb + t * 16 + g * 4 + 2 * odd, S - 1);
           const uint64_t p0 = (((uint64_t)bh * S + qa) * S + mykey) >> 1;
@@ -1041,9 +1098,14 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
           }
           float pd = pr, dp = pa[r];
           if (thr != 0) {
-            const uint32_t bits = (S & 1) ? mift_bits16(seed, ((uint64_t)bh * S + ql) * S + mykey)
-                                          : ((hb[r] >> ((mykey & 1) << 4)) & 0xFFFFu);
-            const bool kp = valid && bits >= thr;
+            bool kp;
+            if (mk) {
+              kp = valid && ((hb[r] >> kc) & 1u);
+            } else {
+              const uint32_t bits = (S & 1) ? mift_bits16(seed, ((uint64_t)bh * S + ql) * S + mykey)
+                                            : ((hb[r] >> ((mykey & 1) << 4)) & 0xFFFFu);
+              kp = valid && bits >= thr;
+            }
             pd = kp ? pr * inv_keep : 0.f;
             dp = kp ? dp * inv_keep : 0.f;
           }
@@ -1075,7 +1137,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
 
 template <typename T, int HD>
 void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int* kvl, int B, int S, int H, float scale,
-                uint64_t seed, uint32_t thr, float inv_keep, hipStream_t st) {
+                uint64_t seed, uint32_t thr, float inv_keep, hipStream_t st, uint16_t* dmask) {
   using G = Geo<HD>;
   // query groups per wave (MIFT_ATTN_QG=1|2).  QG = 2 halves LDS bytes per MFMA but needs
   // 193 VGPRs (2 waves/SIMD vs 3) and measured slower on MI355X (tools/bench_attn.py: OPT-2.7B
@@ -1095,7 +1157,8 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
       attr = true;
     }
     hipLaunchKernelGGL(kern, dim3(B * H), dim3(512), seq_smem, st, (const T*)qkv.data_ptr(), (T*)o.data_ptr(),
-                       lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+                       lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep,
+                       thr != 0 ? dmask : nullptr);
     return;
   }
   if (qg == 2) {
@@ -1114,7 +1177,7 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
 template <typename T, int HD>
 void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
                 at::Tensor& Dv, at::Tensor& dqkv, const int* kvl, int B, int S, int H, float scale, uint64_t seed,
-                uint32_t thr, float inv_keep, hipStream_t st) {
+                uint32_t thr, float inv_keep, hipStream_t st, const uint16_t* dmask) {
   using G = Geo<HD>;
   const int seq_env = attn_seq_mode();
   const int SP = (S + BKV - 1) / BKV * BKV;
@@ -1130,10 +1193,10 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
     }
     hipLaunchKernelGGL(kq, dim3(B * H), dim3(512), seq_dq, st, (const T*)qkv.data_ptr(), (const T*)o.data_ptr(),
                        (const T*)dout.data_ptr(), lse.data_ptr<float>(), Dv.data_ptr<float>(), (T*)dqkv.data_ptr(),
-                       kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+                       kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep, thr != 0 ? dmask : nullptr);
     hipLaunchKernelGGL(kk, dim3(B * H), dim3(512), seq_kv, st, (const T*)qkv.data_ptr(), (const T*)dout.data_ptr(),
                        lse.data_ptr<float>(), Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed,
-                       mift_seed_step(), thr, inv_keep);
+                       mift_seed_step(), thr, inv_keep, thr != 0 ? dmask : nullptr);
     return;
   }
   const int nqt = (S + BQ - 1) / BQ, nkt = (S + BKV - 1) / BKV;
@@ -1149,8 +1212,48 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
 
 }  // namespace
 
+// KEEP BITS: with attention dropout on the whole-sequence path, the forward records every keep
+// decision it draws (1 bit per (query, key) of the causal tiles it visits: [B*H, S, SP/16] uint16,
+// element e of query q = keys 16e..16e+15, 3 MB per distilgpt2 layer) and the backward kernels
+// read the bits instead of re-hashing: the hash is drawn once per element instead of three times.
+// The bits ARE the hash's decisions, so the masks stay bit-identical to the counter-hash contract
+// (common.h) and to the tiled / CPU paths, which keep hashing.
+namespace {
+int64_t keep_bits_elems(int64_t B, int64_t S, int64_t H, int64_t HD, double p) {
+  if (p <= 0.0) return 0;
+  const int64_t SP = (S + BKV - 1) / BKV * BKV;
+  int64_t row = 0;
+  switch (HD) {
+    case 32: row = seq_row_bytes<32>(); break;
+    case 64: row = seq_row_bytes<64>(); break;
+    case 80: row = seq_row_bytes<80>(); break;
+    case 128: row = seq_row_bytes<128>(); break;
+    default: return 0;
+  }
+  const int mode = attn_seq_mode();
+  if (!(mode && 2 * SP * row <= 160 * 1024 && (B * H >= 256 || mode == 2))) return 0;  // tiled path: no record
+  return B * H * S * (SP / 16);
+}
+}  // namespace
+
+std::vector<at::Tensor> mift_attn_fwd_impl(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, int64_t HD,
+                                           double scale, double p, int64_t seed, const c10::optional<at::Tensor>& kv_len,
+                                           bool want_bits);
+
 std::vector<at::Tensor> mift_attn_fwd(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, int64_t HD, double scale,
                                       double p, int64_t seed, const c10::optional<at::Tensor>& kv_len) {
+  return mift_attn_fwd_impl(qkv, B, S, H, HD, scale, p, seed, kv_len, false);
+}
+
+std::vector<at::Tensor> mift_attn_fwd_bits(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, int64_t HD,
+                                           double scale, double p, int64_t seed,
+                                           const c10::optional<at::Tensor>& kv_len) {
+  return mift_attn_fwd_impl(qkv, B, S, H, HD, scale, p, seed, kv_len, true);
+}
+
+std::vector<at::Tensor> mift_attn_fwd_impl(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, int64_t HD,
+                                           double scale, double p, int64_t seed, const c10::optional<at::Tensor>& kv_len,
+                                           bool want_bits) {
   TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && (qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf),
               "attn: bf16/fp16 contiguous qkv");
   TORCH_CHECK(qkv.numel() == B * S * 3 * H * HD, "attn: qkv shape");
@@ -1161,27 +1264,41 @@ std::vector<at::Tensor> mift_attn_fwd(const at::Tensor& qkv, int64_t B, int64_t 
     TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == B, "attn: kv_len int32 [B]");
     kvl = kv_len->data_ptr<int>();
   }
-  if (B * S == 0) return {o, lse};
+  const int64_t nbits = want_bits ? keep_bits_elems(B, S, H, HD, p) : 0;
+  auto bits = at::empty({nbits}, qkv.options().dtype(at::kShort));
+  if (B * S == 0) return {o, lse, bits};
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const uint32_t thr = mift_thr16(p);
   const float inv_keep = p > 0 ? mift_inv_keep(p) : 1.f;
   const bool half = qkv.scalar_type() == at::kHalf;
-#define MIFT_FWD(D)                                                                                         \
-  case D:                                                                                                   \
-    if (half) fwd_launch<fp16, D>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st); \
-    else fwd_launch<bf16, D>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st);      \
+  uint16_t* bp = nbits > 0 ? reinterpret_cast<uint16_t*>(bits.data_ptr()) : nullptr;
+#define MIFT_FWD(D)                                                                                             \
+  case D:                                                                                                       \
+    if (half) fwd_launch<fp16, D>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st, bp); \
+    else fwd_launch<bf16, D>(qkv, o, lse, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, inv_keep, st, bp);      \
     break;
   switch (HD) {
     MIFT_FWD(64) MIFT_FWD(80) MIFT_FWD(128) MIFT_FWD(32)
     default: TORCH_CHECK(false, "attn: unsupported head dim ", HD);
 #undef MIFT_FWD
   }
+  if (want_bits) return {o, lse, bits};
   return {o, lse};
 }
+
+at::Tensor mift_attn_bwd_bits(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
+                              int64_t B, int64_t S, int64_t H, int64_t HD, double scale, double p, int64_t seed,
+                              const c10::optional<at::Tensor>& kv_len, const c10::optional<at::Tensor>& bits);
 
 at::Tensor mift_attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
                          int64_t B, int64_t S, int64_t H, int64_t HD, double scale, double p, int64_t seed,
                          const c10::optional<at::Tensor>& kv_len) {
+  return mift_attn_bwd_bits(dout, qkv, o, lse, B, S, H, HD, scale, p, seed, kv_len, c10::nullopt);
+}
+
+at::Tensor mift_attn_bwd_bits(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
+                              int64_t B, int64_t S, int64_t H, int64_t HD, double scale, double p, int64_t seed,
+                              const c10::optional<at::Tensor>& kv_len, const c10::optional<at::Tensor>& bits) {
   TORCH_CHECK(dout.is_contiguous() && o.is_contiguous(), "attn_bwd: contiguous");
   auto dqkv = at::empty_like(qkv);
   auto Dv = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
@@ -1192,12 +1309,19 @@ at::Tensor mift_attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at
   const float inv_keep = p > 0 ? mift_inv_keep(p) : 1.f;
   TORCH_CHECK(dout.scalar_type() == qkv.scalar_type() && o.scalar_type() == qkv.scalar_type(), "attn_bwd: dtype");
   const bool half = qkv.scalar_type() == at::kHalf;
+  // the forward's keep-bit record is used only when it exists for THIS launch geometry (the
+  // backward takes the whole-sequence path exactly when the forward did); otherwise re-hash
+  const uint16_t* bp = nullptr;
+  if (bits && bits->numel() > 0) {
+    TORCH_CHECK(bits->is_cuda() && bits->scalar_type() == at::kShort && bits->is_contiguous(), "attn_bwd: keep bits");
+    if (bits->numel() == keep_bits_elems(B, S, H, HD, p)) bp = reinterpret_cast<const uint16_t*>(bits->data_ptr());
+  }
 #define MIFT_BWD(D)                                                                                          \
   case D:                                                                                                    \
     if (half) bwd_launch<fp16, D>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr, \
-                                  inv_keep, st);                                                             \
+                                  inv_keep, st, bp);                                                         \
     else bwd_launch<bf16, D>(dout, qkv, o, lse, Dv, dqkv, kvl, B, S, H, (float)scale, (uint64_t)seed, thr,      \
-                             inv_keep, st);                                                                  \
+                             inv_keep, st, bp);                                                              \
     break;
   switch (HD) {
     MIFT_BWD(64) MIFT_BWD(80) MIFT_BWD(128) MIFT_BWD(32)

@@ -70,6 +70,12 @@ std::vector<at::Tensor> mift_attn_fwd(const at::Tensor& qkv, int64_t B, int64_t 
 at::Tensor mift_attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
                          int64_t B, int64_t S, int64_t H, int64_t HD, double scale, double p, int64_t seed,
                          const c10::optional<at::Tensor>& kv_len);
+std::vector<at::Tensor> mift_attn_fwd_bits(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, int64_t HD,
+                                           double scale, double p, int64_t seed,
+                                           const c10::optional<at::Tensor>& kv_len);
+at::Tensor mift_attn_bwd_bits(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
+                              int64_t B, int64_t S, int64_t H, int64_t HD, double scale, double p, int64_t seed,
+                              const c10::optional<at::Tensor>& kv_len, const c10::optional<at::Tensor>& bits);
 
 // ---- K12 decode attention over a KV cache (kernels/decode.hip)
 at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
@@ -85,6 +91,8 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
   m.def("pack_lora_all", &mift_pack_lora_all, "pack every adapter's 16-bit operands from the fp32 arena"); \
   m.def("attn_fwd", &mift_attn_fwd, "causal flash attention fwd on fused qkv -> (o, lse)"); \
   m.def("attn_bwd", &mift_attn_bwd, "causal flash attention bwd -> dqkv"); \
+  m.def("attn_fwd_bits", &mift_attn_fwd_bits, "attn fwd that also records its dropout keep bits -> (o, lse, bits)"); \
+  m.def("attn_bwd_bits", &mift_attn_bwd_bits, "attn bwd reading the forward's keep bits -> dqkv"); \
   m.def("gemm_nt", &mift_gemm_nt, "C = epi(A @ B^T [+ A2 @ B2^T]) MFMA bf16/fp16"); \
   m.def("lmhead_fwd", &mift_lmhead_fwd, "fused LM head + CE fwd -> (E, stats, lse, loss, zlab)"); \
   m.def("lmhead_dgrad", &mift_lmhead_dgrad, "fused LM head + CE dgrad -> dX (no dlogits)"); \

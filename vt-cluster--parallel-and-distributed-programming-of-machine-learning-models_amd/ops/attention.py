@@ -6,6 +6,8 @@ and returns [B, S, H*hd].  GPU tensors run the gfx950 flash-attention
 kernels (csrc/kernels/attention.hip) when available for the head dim;
 otherwise (CPU) the reference path.
 """
+import os
+
 import torch
 import torch.nn.functional as Fnn
 
@@ -19,20 +21,28 @@ def _split(qkv, B, S, H, hd):
 
 
 class _FlashAttn(torch.autograd.Function):
+    """With dropout the forward also returns its keep-bit record (whole-sequence kernels, see
+    KEEP BITS in csrc/kernels/attention.hip) and the backward reads it instead of re-hashing
+    (``MIFT_ATTN_BITS=0``: re-hash, for A/B measurements; read per call, i.e. at graph capture)."""
+
     @staticmethod
     def forward(ctx, qkv, B, S, H, hd, scale, p, seed, kv_len):
         qkv = qkv.contiguous()
-        o, lse = C().attn_fwd(qkv, B, S, H, hd, float(scale), float(p), int(seed), kv_len)
-        ctx.save_for_backward(qkv, o, lse, kv_len if kv_len is not None else torch.empty(0))
+        if p > 0 and os.environ.get("MIFT_ATTN_BITS", "1") != "0":
+            o, lse, bits = C().attn_fwd_bits(qkv, B, S, H, hd, float(scale), float(p), int(seed), kv_len)
+        else:
+            (o, lse), bits = C().attn_fwd(qkv, B, S, H, hd, float(scale), float(p), int(seed), kv_len), None
+        ctx.save_for_backward(qkv, o, lse, kv_len if kv_len is not None else torch.empty(0),
+                              bits if bits is not None else torch.empty(0))
         ctx.meta = (B, S, H, hd, scale, p, seed, kv_len is not None)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse, kv_len = ctx.saved_tensors
+        qkv, o, lse, kv_len, bits = ctx.saved_tensors
         B, S, H, hd, scale, p, seed, has_len = ctx.meta
-        dqkv = C().attn_bwd(do.contiguous(), qkv, o, lse, B, S, H, hd, float(scale), float(p), int(seed),
-                            kv_len if has_len else None)
+        dqkv = C().attn_bwd_bits(do.contiguous(), qkv, o, lse, B, S, H, hd, float(scale), float(p), int(seed),
+                                 kv_len if has_len else None, bits if bits.numel() else None)
         return dqkv, None, None, None, None, None, None, None, None
 
 
