@@ -272,6 +272,18 @@ MIFT_HD void mift_keep4_hm(uint64_t seed, uint32_t hm, uint64_t idx0, uint32_t t
   k[0] = (h0 & 0xFFFFu) >= thr; k[1] = (h0 >> 16) >= thr;
   k[2] = (h1 & 0xFFFFu) >= thr; k[3] = (h1 >> 16) >= thr;
 }
+// AND-masks of 8 consecutive packed 16-bit values at element idx0 (even): w[e] keeps element pair
+// (2e, 2e+1) as 0x0000FFFF / 0xFFFF0000 halves.  Same keep decisions as mift_keep8; for kernels that
+// apply the 1/(1-p) scale once to an fp32 accumulator instead of per element (hz: the pair index's
+// high word is 0, hm0 = mift_hmix(seed, 0) hoisted by the caller).
+MIFT_HD void mift_andmask8(uint64_t seed, uint32_t hm0, bool hz, uint64_t idx0, uint32_t thr, uint32_t* w) {
+  const uint64_t pr = idx0 >> 1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t h = hz ? mift_hash_lo(seed, hm0, (uint32_t)pr + e) : mift_hash_pair(seed, pr + e);
+    w[e] = ((h & 0xFFFFu) >= thr ? 0x0000FFFFu : 0u) | ((h >> 16) >= thr ? 0xFFFF0000u : 0u);
+  }
+}
 // bare v_exp_f32 (no denormal range handling; softmax inputs are <= 0 or -inf)
 MIFT_HD float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 

@@ -96,6 +96,10 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict_
   constexpr int UNR = MT == 1 ? 8 : 4;
   const int per = (nks - kb0 + NW - 1) / NW;
   const int kbeg = kb0 + wave * per, kend = min(nks, kbeg + per);
+  // LoRA-input dropout: kept elements enter the MFMA unscaled (AND on packed pairs); the host folds
+  // 1/(1-p) into alpha, applied once to the fp32 sums
+  const bool hz = (uint64_t)M * K < (1ull << 33);
+  const uint32_t hm0 = mift_hmix(seed, 0);
   for (int ks0 = kbeg; ks0 < kend; ks0 += UNR) {
     short8 ra[UNR][MT], rb[UNR][NTI];
 #pragma unroll
@@ -115,17 +119,12 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict_
       for (int i = 0; i < MT; ++i) {
         short8 v = ra[u][i];
         if (thr != 0) {
-          bool kp[8];
-          mift_keep8(seed, (uint64_t)rows[i] * K + col, thr, kp);
+          uint32_t w[4], km[4];
+          __builtin_memcpy(w, &v, 16);
+          mift_andmask8(seed, hm0, hz, (uint64_t)rows[i] * K + col, thr, km);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            short s = v[e];
-            T t;
-            __builtin_memcpy(&t, &s, 2);
-            t = kp[e] ? (T)((float)t * inv_keep) : (T)0.f;
-            __builtin_memcpy(&s, &t, 2);
-            v[e] = s;
-          }
+          for (int e = 0; e < 4; ++e) w[e] &= km[e];
+          __builtin_memcpy(&v, w, 16);
         }
         __builtin_memcpy(&a[i], &v, 16);
       }
@@ -352,6 +351,157 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const WgArgs args) {
     }
 }
 
+// v2 (default; MIFT_WGRAD_V=1 selects the kernel above): the same tiles and LDS images, but two
+// register sets of NB-step load groups alternate, so group g+2's global loads are issued as soon as
+// group g has been written to LDS and group g+1's have had a whole iteration to land (the v1 loop
+// kept ONE group in flight per block: each group paid the full load latency).  NQT = 1 when every
+// slot of the launch lives in columns [0, 16) (rank <= 16, one adapter per input): one MFMA per
+// 32-row step instead of two and half the Y bytes.
+template <typename T, int NQT>
+__global__ __launch_bounds__(256) void lora_wgrad2_kernel(const WgArgs args) {
+  int pi = 0;
+#pragma unroll 1
+  while (pi + 1 < args.np && (int)blockIdx.x >= args.p[pi + 1].blk0) ++pi;
+  const WgProb& pr = args.p[pi];
+  const T* __restrict__ X = reinterpret_cast<const T*>(pr.X);
+  const T* __restrict__ Y = reinterpret_cast<const T*>(pr.Y);
+  const int M = pr.M, P = pr.P, ldx = pr.ldx, rows_per_block = pr.rows;
+  const uint32_t thr = pr.thr;
+  const float inv_keep = pr.inv_keep;
+  const uint64_t seed = mift_seed(pr.seed, args.sstep);
+  const int lb = blockIdx.x - pr.blk0;
+  constexpr int NB = 4;
+  constexpr int YT = NQT == 2 ? 128 : 64;  // threads loading Y (16 B each: 4 or 2 chunks per 32-col row)
+  __shared__ __attribute__((aligned(16))) char Xs[NB][32 * XS];
+  __shared__ __attribute__((aligned(16))) char Ys[NB][32 * YS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int ntp = P / 64;
+  const int pt = lb % ntp, ms = lb / ntp;
+  const int p0 = pt * 64;
+  const int mbeg = ms * rows_per_block;
+  const int mend = min(mbeg + rows_per_block, M);
+  MIFT_ASSERT(P % 64 == 0 && mbeg < M);
+  float4_ acc[NQT];
+#pragma unroll
+  for (int c = 0; c < NQT; ++c) acc[c] = float4_{0.f, 0.f, 0.f, 0.f};
+
+  const int xr = tid >> 3, xc = tid & 7;
+  const int yr = NQT == 2 ? (tid & 127) >> 2 : (tid & 63) >> 1, yc = NQT == 2 ? tid & 3 : tid & 1;
+  short8 xa[NB], ya[NB], xb[NB], yb[NB];
+  auto gload = [&](short8 (&xv)[NB], short8 (&yv)[NB], int m0g) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      const int m = m0g + 32 * s;
+      const int gm = min(m + xr, M - 1);
+      xv[s] = *reinterpret_cast<const short8*>(X + (int64_t)gm * ldx + p0 + xc * 8);
+      if (tid < YT) {
+        const int gy = min(m + yr, M - 1);
+        yv[s] = *reinterpret_cast<const short8*>(Y + (int64_t)gy * 32 + yc * 8);
+      }
+    }
+  };
+  // LoRA-input dropout on X: the kept elements enter the MFMA unscaled (a bitwise AND on the packed
+  // 16-bit pairs) and the 1/(1-p) factor is applied to the fp32 accumulators once at the end —
+  // the per-element unpack/scale/round/repack cost as much VALU as the hash itself (the masked dA
+  // problems were VALU-issue bound: +28 % over unmasked ones).  The pair hashes share one hoisted
+  // high-word mix (element indices < 2^33).
+  const bool hz = (uint64_t)M * P < (1ull << 33);
+  const uint32_t hm0 = mift_hmix(seed, 0);
+  auto lstore = [&](short8 (&xv)[NB], short8 (&yv)[NB], int m0g) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      const int m = m0g + 32 * s;
+      const bool valid = (m + xr) < mend;
+      short8 v = xv[s];
+      if (!valid) {
+        v = short8{0, 0, 0, 0, 0, 0, 0, 0};
+      } else if (thr != 0) {
+        uint32_t w[4], km[4];
+        __builtin_memcpy(w, &v, 16);
+        mift_andmask8(seed, hm0, hz, (uint64_t)(m + xr) * P + p0 + xc * 8, thr, km);  // 8-aligned columns
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] &= km[e];
+        __builtin_memcpy(&v, w, 16);
+      }
+      *reinterpret_cast<short8*>(Xs[s] + xr * XS + xc * 16) = v;
+      if (tid < YT) {
+        short8 w = yv[s];
+        if ((m + yr) >= mend) w = short8{0, 0, 0, 0, 0, 0, 0, 0};
+        *reinterpret_cast<short8*>(Ys[s] + yr * YS + yc * 16) = w;
+      }
+    }
+  };
+  const int q4 = li >> 2, p4 = li & 3;
+  const int rowA = 4 * g + q4;
+  const int xoff = rowA * XS + (wave * 16 + p4 * 4) * 2;
+  const int yoff0 = rowA * YS + (0 * 16 + p4 * 4) * 2;
+  const int yoff1 = rowA * YS + (1 * 16 + p4 * 4) * 2;
+  auto compute = [&](int mg) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      if (mg + 32 * s >= mend) break;
+      const char* xbp = Xs[s];
+      const char* ybp = Ys[s];
+      v4s a0 = tr_read<T>(xbp, xoff), a1 = tr_read<T>(xbp, xoff + 16 * XS);
+      v4s b00 = tr_read<T>(ybp, yoff0), b01 = tr_read<T>(ybp, yoff0 + 16 * YS);
+      frag_t<T> af, bf0;
+      short8 t = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      __builtin_memcpy(&af, &t, 16);
+      short8 u = {b00[0], b00[1], b00[2], b00[3], b01[0], b01[1], b01[2], b01[3]};
+      __builtin_memcpy(&bf0, &u, 16);
+      acc[0] = mfma16<T>(af, bf0, acc[0]);
+      if constexpr (NQT == 2) {
+        v4s b10 = tr_read<T>(ybp, yoff1), b11 = tr_read<T>(ybp, yoff1 + 16 * YS);
+        frag_t<T> bf1;
+        short8 w = {b10[0], b10[1], b10[2], b10[3], b11[0], b11[1], b11[2], b11[3]};
+        __builtin_memcpy(&bf1, &w, 16);
+        acc[1] = mfma16<T>(af, bf1, acc[1]);
+      }
+    }
+  };
+  constexpr int GR = 32 * NB;  // rows per load group
+  if (mbeg < mend) gload(xa, ya, mbeg);
+  if (mbeg + GR < mend) gload(xb, yb, mbeg + GR);
+  for (int mg = mbeg; mg < mend; mg += 2 * GR) {
+    __syncthreads();
+    lstore(xa, ya, mg);
+    __syncthreads();
+    if (mg + 2 * GR < mend) gload(xa, ya, mg + 2 * GR);
+    compute(mg);
+    if (mg + GR >= mend) break;
+    __syncthreads();
+    lstore(xb, yb, mg + GR);
+    __syncthreads();
+    if (mg + 3 * GR < mend) gload(xb, yb, mg + 3 * GR);
+    compute(mg + GR);
+  }
+  if (thr != 0) {
+#pragma unroll
+    for (int c = 0; c < NQT; ++c) acc[c] *= inv_keep;
+  }
+  float* out = args.out;
+#pragma unroll
+  for (int c = 0; c < NQT; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t pp = p0 + wave * 16 + g * 4 + r;
+      const int q = c * 16 + li;
+      if (pr.mode == 0) {
+        atomicAdd(out + pr.slot[0].offset + pp * 32 + q, acc[c][r]);
+        continue;
+      }
+#pragma unroll 1
+      for (int si = 0; si < pr.nslot; ++si) {
+        const WgSlot& sl = pr.slot[si];
+        if (q >= sl.qoff && q < sl.qoff + sl.rank)
+          atomicAdd(out + sl.offset + (pr.mode == 1 ? pp * sl.rank + (q - sl.qoff) : (int64_t)(q - sl.qoff) * P + pp),
+                    acc[c][r]);
+      }
+    }
+}
+
 }  // namespace
 
 at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed,
@@ -392,7 +542,7 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   auto go = [&](auto tt) {
     using T = decltype(tt);
     auto args = std::make_tuple((const T*)x.data_ptr(), (const T*)w.data_ptr(), (T*)out.data_ptr(), M, K,
-                                (int)x.stride(0), (float)alpha, (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
+                                (int)x.stride(0), (float)alpha * ik, (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
     auto launch = [&](auto kern) {
       std::apply([&](auto... a) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a...); }, args);
     };
@@ -406,9 +556,9 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   if (KS > 1) {
     const int rg = (int)(((int64_t)M * 32 / 8 + 255) / 256);
     if (x.scalar_type() == at::kBFloat16)
-      lora_proj_reduce<bf16><<<rg, 256, 0, st>>>(ws, (bf16*)out.data_ptr(), M, KS, (float)alpha);
+      lora_proj_reduce<bf16><<<rg, 256, 0, st>>>(ws, (bf16*)out.data_ptr(), M, KS, (float)alpha * ik);
     else
-      lora_proj_reduce<fp16><<<rg, 256, 0, st>>>(ws, (fp16*)out.data_ptr(), M, KS, (float)alpha);
+      lora_proj_reduce<fp16><<<rg, 256, 0, st>>>(ws, (fp16*)out.data_ptr(), M, KS, (float)alpha * ik);
   }
   return out;
 }
@@ -430,7 +580,20 @@ void launch_wgrad(WgArgs& args, hipStream_t st) {
     p.blk0 = blk;
     blk += (p.P / 64) * ((p.M + p.rows - 1) / p.rows);
   }
-  if (blk > 0) lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
+  if (blk == 0) return;
+  const char* ve = getenv("MIFT_WGRAD_V");  // A/B knob, read per launch: 1 = the v1 kernel
+  if (ve != nullptr && atoi(ve) == 1) {
+    lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
+    return;
+  }
+  bool narrow = true;  // every slot within columns [0, 16)
+  for (int i = 0; i < args.np; ++i) {
+    if (args.p[i].mode == 0) narrow = false;
+    for (int si = 0; si < args.p[i].nslot; ++si)
+      if (args.p[i].slot[si].qoff + args.p[i].slot[si].rank > 16) narrow = false;
+  }
+  if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
+  else lora_wgrad2_kernel<T, 2><<<blk, 256, 0, st>>>(args);
 }
 }  // namespace
 

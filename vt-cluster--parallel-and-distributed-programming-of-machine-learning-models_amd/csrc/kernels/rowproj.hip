@@ -13,8 +13,9 @@
 //                  (grad of attn.c_proj / mlp.c_proj outputs -> dT)
 //
 // Numerics match lora_proj: the projection consumes the 16-bit value the
-// consumer GEMM sees (y rounded to T), the LoRA-input dropout value is
-// rounded to T after scaling, accumulation is fp32, the output rounded once.
+// consumer GEMM sees (y rounded to T); dropped elements are zeroed and the
+// 1/(1-p) scale is applied once to the fp32 sums (folded into alpha by the
+// host), accumulation is fp32, the output rounded once.
 //
 // Cross-lane reduction of the LR per-lane partial sums: a reduce-scatter
 // butterfly (each xor step sends the half of the partials the lane does not
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void ln_fwd_proj_kernel(const T* __restrict__ 
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         const float yb = rnd<T>(o[i]);
-        dv[i] = thr != 0 ? (kp[i] ? rnd<T>(yb * inv_keep) : 0.f) : yb;
+        dv[i] = kp[i] ? yb : 0.f;  // 1/(1-p) folded into alpha by the host
       }
 #pragma unroll
       for (int j = 0; j < LR; ++j) {
@@ -256,12 +257,12 @@ std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::
           ln_fwd_proj_kernel<T, float, NIT, LR><<<(M + 3) / 4, 256, 0, st>>>(
               (const T*)x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), (T*)y.data_ptr(),
               mean.data_ptr<float>(), rstd.data_ptr<float>(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, D,
-              (float)eps, (float)alpha, (uint64_t)seed, mift_seed_step(), thr, inv);
+              (float)eps, (float)alpha * inv, (uint64_t)seed, mift_seed_step(), thr, inv);
         else
           ln_fwd_proj_kernel<T, T, NIT, LR><<<(M + 3) / 4, 256, 0, st>>>(
               (const T*)x.data_ptr(), (const T*)w.data_ptr(), (const T*)b.data_ptr(), (T*)y.data_ptr(),
               mean.data_ptr<float>(), rstd.data_ptr<float>(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, D,
-              (float)eps, (float)alpha, (uint64_t)seed, mift_seed_step(), thr, inv);
+              (float)eps, (float)alpha * inv, (uint64_t)seed, mift_seed_step(), thr, inv);
       });
     });
   };
