@@ -54,6 +54,38 @@ MIFT_HD void st4(T* p, const float* o) {
 template <typename T>
 MIFT_HD float rnd(float v) { return (float)(T)v; }
 
+// acc + x·w over 4 packed 16-bit values with two v_dot2_f32_{bf16,f16} (no unpacking to fp32: the
+// per-element converts of the weight rows were most of these kernels' vector instructions)
+typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+typedef _Float16 fp16x2_ __attribute__((ext_vector_type(2)));
+template <typename T>
+MIFT_HD float dot4(short4_ x, short4_ w, float acc) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    bf16x2_ x0, x1, w0, w1;
+    __builtin_memcpy(&x0, &x, 4);
+    __builtin_memcpy(&x1, reinterpret_cast<const char*>(&x) + 4, 4);
+    __builtin_memcpy(&w0, &w, 4);
+    __builtin_memcpy(&w1, reinterpret_cast<const char*>(&w) + 4, 4);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(x0, w0, acc, false);
+    return __builtin_amdgcn_fdot2_f32_bf16(x1, w1, acc, false);
+  } else {
+    fp16x2_ x0, x1, w0, w1;
+    __builtin_memcpy(&x0, &x, 4);
+    __builtin_memcpy(&x1, reinterpret_cast<const char*>(&x) + 4, 4);
+    __builtin_memcpy(&w0, &w, 4);
+    __builtin_memcpy(&w1, reinterpret_cast<const char*>(&w) + 4, 4);
+    acc = __builtin_amdgcn_fdot2(x0, w0, acc, false);
+    return __builtin_amdgcn_fdot2(x1, w1, acc, false);
+  }
+}
+template <typename T>
+MIFT_HD short4_ pack4(const float* o) {
+  short4_ v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { T t = (T)o[i]; short s; __builtin_memcpy(&s, &t, 2); v[i] = s; }
+  return v;
+}
+
 // acc[0..LR) partial sums per lane -> out[row, 0..32) (cols >= LR zero), times alpha
 template <typename T, int LR>
 MIFT_HD void reduce_store(float (&acc)[LR], T* out_row, int lane, float alpha) {
@@ -132,22 +164,17 @@ __global__ __launch_bounds__(256) void ln_fwd_proj_kernel(const T* __restrict__ 
       ldw4<W>(b + c, bv);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) o[i] = (v[it][i] - mean) * rstd * wv[i] + bv[i];
-      st4<T>(yr + c, o);
-      bool kp[VEC] = {true, true, true, true};
-      if (thr != 0) mift_keep4(seed, (uint64_t)row * D + c, thr, kp);
-      float dv[VEC];
+      short4_ yb = pack4<T>(o);  // the 16-bit y the consumer GEMM sees
+      *reinterpret_cast<short4_*>(yr + c) = yb;
+      if (thr != 0) {  // dropped elements zeroed; 1/(1-p) folded into alpha by the host
+        bool kp[VEC];
+        mift_keep4(seed, (uint64_t)row * D + c, thr, kp);
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        const float yb = rnd<T>(o[i]);
-        dv[i] = kp[i] ? yb : 0.f;  // 1/(1-p) folded into alpha by the host
+        for (int i = 0; i < VEC; ++i) yb[i] = kp[i] ? yb[i] : (short)0;
       }
 #pragma unroll
-      for (int j = 0; j < LR; ++j) {
-        float a[VEC];
-        ld4<T>(pw + (size_t)j * D + c, a);
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[j] += dv[i] * a[i];
-      }
+      for (int j = 0; j < LR; ++j)
+        acc[j] = dot4<T>(yb, *reinterpret_cast<const short4_*>(pw + (size_t)j * D + c), acc[j]);
     }
   }
   if (lane == 0) {
@@ -174,24 +201,20 @@ __global__ __launch_bounds__(256) void mask_proj_kernel(const T* __restrict__ x,
   for (int it = 0; it < NIT; ++it) {
     const int c = (it * 64 + lane) * VEC;
     if (c < D) {
-      float v[VEC];
-      ld4<T>(xr + c, v);
+      short4_ yb = *reinterpret_cast<const short4_*>(xr + c);
       if (thr != 0) {
+        float v[VEC];
+        ld4<T>(xr + c, v);
         bool kp[VEC];
         mift_keep4(seed, (uint64_t)row * D + c, thr, kp);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) v[i] = kp[i] ? v[i] * inv_keep : 0.f;
-        st4<T>(yr + c, v);
+        yb = pack4<T>(v);  // the 16-bit y written out is the one projected
+        *reinterpret_cast<short4_*>(yr + c) = yb;
       }
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) v[i] = rnd<T>(v[i]);
-#pragma unroll
-      for (int j = 0; j < LR; ++j) {
-        float a[VEC];
-        ld4<T>(pw + (size_t)j * D + c, a);
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[j] += v[i] * a[i];
-      }
+      for (int j = 0; j < LR; ++j)
+        acc[j] = dot4<T>(yb, *reinterpret_cast<const short4_*>(pw + (size_t)j * D + c), acc[j]);
     }
   }
   reduce_store<T, LR>(acc, pout + (size_t)row * 32, lane, alpha);
