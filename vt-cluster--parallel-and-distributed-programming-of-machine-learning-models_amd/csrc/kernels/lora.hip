@@ -70,7 +70,7 @@ template <typename T, int NW, int MT, int NTI>
 __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict__ X, const T* __restrict__ W,
                                                         T* __restrict__ out, int M, int K, int ldx, float alpha,
                                                         uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep, int KS,
-                                                        float* __restrict__ ws) {
+                                                        float* __restrict__ ws, int wrows) {
   seed = mift_seed(seed, sstep);
   constexpr int RB = 16 * MT;  // rows per block
   __shared__ float red[NW][RB][33];
@@ -107,8 +107,12 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict_
       const int col = min(ks0 + u, nks - 1) * 32 + g * 8;
 #pragma unroll
       for (int i = 0; i < MT; ++i) ra[u][i] = *reinterpret_cast<const short8*>(X + (int64_t)rows[i] * ldx + col);
+      // rows >= wrows of W are zero padding: not fetched (the rank-8 adapters' 16-row tile is half
+      // padding, and every block re-reads W from L2)
 #pragma unroll
-      for (int j = 0; j < NTI; ++j) rb[u][j] = *reinterpret_cast<const short8*>(W + (int64_t)(j * 16 + fr) * K + col);
+      for (int j = 0; j < NTI; ++j)
+        rb[u][j] = j * 16 + fr < wrows ? *reinterpret_cast<const short8*>(W + (int64_t)(j * 16 + fr) * K + col)
+                                       : short8{0, 0, 0, 0, 0, 0, 0, 0};
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
@@ -542,7 +546,8 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   auto go = [&](auto tt) {
     using T = decltype(tt);
     auto args = std::make_tuple((const T*)x.data_ptr(), (const T*)w.data_ptr(), (T*)out.data_ptr(), M, K,
-                                (int)x.stride(0), (float)alpha * ik, (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws);
+                                (int)x.stride(0), (float)alpha * ik, (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws,
+                                (int)rows);
     auto launch = [&](auto kern) {
       std::apply([&](auto... a) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a...); }, args);
     };
