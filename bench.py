@@ -125,9 +125,15 @@ def main():
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
+    trace = os.environ.get("MIFT_BENCH_TRACE") == "1"  # diagnostics: per-step host ms to stderr
+    sync_every = int(os.environ.get("MIFT_BENCH_SYNC", "0"))  # diagnostics: host sync every k steps
     t0 = time.perf_counter()
     for i in range(a.warmup, total_steps):
         run(i)
+        if trace or (sync_every and (i + 1) % sync_every == 0):
+            torch.cuda.synchronize()
+        if trace:
+            print(f"step {i} {(time.perf_counter() - t0) * 1000:.2f}", file=sys.stderr)
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()

@@ -149,7 +149,7 @@ def main(argv=None, defaults=None):
                        output_dir=save_dir, resume=args.resume,
                        recompute=bool(args.gradient_checkpointing) or mcfg.activation_checkpointing,
                        step_log=args.step_log, seed=args.seed, bucket_mb=mcfg.bucket_mb, graph=mcfg.graph,
-                       consistency_every=mcfg.consistency_every, max_grad_norm=mcfg.gradient_clipping,
+                       consistency_every=mcfg.consistency_every, max_inflight_steps=mcfg.max_inflight_steps, max_grad_norm=mcfg.gradient_clipping,
                        weight_decay=mcfg.weight_decay, profile_dir=args.profile, profile_steps=args.profile_steps)
     trainer = Trainer(model, batcher, tcfg, ctx)
     logs.log("Trainer setup", time.perf_counter() - t0)

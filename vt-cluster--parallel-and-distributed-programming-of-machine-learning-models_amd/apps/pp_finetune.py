@@ -171,7 +171,7 @@ def main(argv=None):
                        weight_decay=ds.weight_decay, max_grad_norm=ds.gradient_clipping, logging_steps=args.log_every,
                        step_log="none", max_steps=args.max_steps, seed=args.seed, zero_stage=zero,
                        recompute=bool(args.gradient_checkpointing) or ds.activation_checkpointing,
-                       bucket_mb=ds.bucket_mb, graph=ds.graph, consistency_every=ds.consistency_every,
+                       bucket_mb=ds.bucket_mb, graph=ds.graph, consistency_every=ds.consistency_every, max_inflight_steps=ds.max_inflight_steps,
                        save_steps=args.save_steps,
                        output_dir=os.path.join(args.out_root, "checkpoints") if args.save_steps else None,
                        resume=args.resume, profile_dir=args.profile, profile_steps=args.profile_steps)

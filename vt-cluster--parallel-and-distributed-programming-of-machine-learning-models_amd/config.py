@@ -19,7 +19,7 @@ Reference: P2 loads a DeepSpeed JSON (``--ds_cfg``,
   (fused | blas), ``bucket_mb`` (DP all-reduce bucket), ``pp_partition`` (uniform | balanced),
   ``pp_schedule`` (1f1b), ``micro_batch`` (GPU micro-batch regrouping), ``side_stream``
   (LoRA weight grads on a second stream), ``comm_timeout_s`` (collective watchdog),
-  ``consistency_every`` (replica checksum period);
+  ``consistency_every`` (replica checksum period), ``max_inflight_steps`` (host run-ahead bound);
 * anything else is an error unless ``mift.strict`` is false (then a warning).
 
 ``MiftConfig.apply_env()`` exports the process-wide toggles (``MIFT_KERNELS``, ``MIFT_GRAPH``,
@@ -49,7 +49,7 @@ _NO_EFFECT = {
     "wall_clock_breakdown": "phase timers are always on (timing_rank*.log)",
 }
 _MIFT_KEYS = {"kernels", "graph", "lmhead", "bucket_mb", "pp_partition", "pp_schedule", "micro_batch", "side_stream",
-              "comm_timeout_s", "consistency_every", "strict"}
+              "comm_timeout_s", "consistency_every", "max_inflight_steps", "strict"}
 
 
 @dataclass
@@ -80,6 +80,7 @@ class MiftConfig:
     side_stream: Optional[bool] = None
     comm_timeout_s: Optional[int] = None
     consistency_every: int = 0
+    max_inflight_steps: int = 2
     strict: bool = True
     # --- provenance ---
     source: Optional[str] = None
@@ -142,6 +143,7 @@ class MiftConfig:
         c.side_stream = m.get("side_stream")
         c.comm_timeout_s = m.get("comm_timeout_s")
         c.consistency_every = int(m.get("consistency_every", 0))
+        c.max_inflight_steps = int(m.get("max_inflight_steps", 2))
         for name, val, ok in [("graph", c.graph, ("auto", "on", "off")), ("lmhead", c.lmhead, ("fused", "blas")),
                               ("pp_partition", c.pp_partition, ("uniform", "balanced")),
                               ("pp_schedule", c.pp_schedule, ("1f1b",))]:
