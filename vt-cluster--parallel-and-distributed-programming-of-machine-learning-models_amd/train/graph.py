@@ -42,8 +42,6 @@ class GraphedStep:
         self.graphs = {}      # signature -> dict(graph, static, steps_t, loss)
         self.seen = set()     # signatures already run eagerly once (warm-up)
         self.max_graphs = max_graphs
-        dev = trainer.device
-        self.inv_ntok = torch.ones(1, dtype=torch.float32, device=dev)
         self.pool = None
 
     @staticmethod
@@ -73,7 +71,7 @@ class GraphedStep:
         tr, model = self.tr, self.tr.model
         C = _C()
         # the scaled upstream gradient seeds backward directly (no ones-fill + multiply kernels)
-        gscale = (tr.opt.loss_scale_t * self.inv_ntok).reshape(())
+        gscale = (tr.opt.loss_scale_t * ent["inv_ntok"]).reshape(())
         for i in range(n):
             C.set_seed_step(ent["steps_t"][i:i + 1])
             mb = ent["static"][i]
@@ -88,13 +86,38 @@ class GraphedStep:
                 ent["loss"].add_(loss_sum.detach())
         C.set_seed_step(None)
 
+    # Per-step inputs of a replay — every micro-batch tensor, the micro-step counters and 1/tokens —
+    # live in ONE device buffer that one async copy refreshes from a ring of pinned staging buffers
+    # (host-side packing): one SDMA transfer per step instead of three per micro-batch + two scalar
+    # kernels (the separate transfers left a ~40 us hole at the top of every replayed step).
+    _RING = 4
+
+    def _layout(self, mbs):
+        items, off = [], 0
+        for i, mb in enumerate(mbs):
+            for k, v in sorted(mb.items()):
+                n = v.numel() * v.element_size()
+                items.append((i, k, off, n, v.dtype, tuple(v.shape)))
+                off = (off + n + 255) // 256 * 256
+        steps_off = off
+        off = (off + 8 * len(mbs) + 255) // 256 * 256
+        return items, steps_off, off, off + 4  # ..., inv_ntok offset, total bytes
+
     def _capture(self, sig, mbs):
         tr, model = self.tr, self.tr.model
         dev = tr.device
-        static = [{k: torch.empty_like(v, device=dev) for k, v in mb.items()} for mb in mbs]
+        items, steps_off, inv_off, total = self._layout(mbs)
+        dbuf = torch.zeros(total, dtype=torch.uint8, device=dev)
+        static = [dict() for _ in mbs]
+        for i, k, off, n, dt, shp in items:
+            static[i][k] = dbuf[off:off + n].view(dt).view(shp)
+        pin = torch.cuda.is_available()
         ent = {"static": static, "loss": torch.zeros((), dtype=torch.float32, device=dev),
-               "steps_t": torch.zeros(len(mbs), dtype=torch.int64, device=dev),
-               "arange": torch.arange(1, len(mbs) + 1, dtype=torch.int64, device=dev)}
+               "steps_t": dbuf[steps_off:steps_off + 8 * len(mbs)].view(torch.int64),
+               "inv_ntok": dbuf[inv_off:inv_off + 4].view(torch.float32),
+               "dbuf": dbuf, "items": items, "steps_off": steps_off, "inv_off": inv_off,
+               "stage": [torch.zeros(total, dtype=torch.uint8, pin_memory=pin) for _ in range(self._RING)],
+               "stage_ev": [None] * self._RING, "slot": 0}
         for i, mb in enumerate(mbs):
             for k, v in mb.items():
                 static[i][k].copy_(v)
@@ -136,13 +159,22 @@ class GraphedStep:
         fresh = ent is None
         if fresh:
             ent = self._capture(sig, mbs)
-        else:
-            for i, mb in enumerate(mbs):
-                for k, v in mb.items():
-                    ent["static"][i][k].copy_(v, non_blocking=True)
-        self.inv_ntok.fill_(1.0 / float(ntok))
         n = len(mbs)
-        torch.add(ent["arange"], model.micro_step, out=ent["steps_t"])
+        slot = ent["slot"]
+        ent["slot"] = (slot + 1) % self._RING
+        ev = ent["stage_ev"][slot]
+        if ev is not None:
+            ev.synchronize()  # that staging buffer's previous upload has been consumed
+        st = ent["stage"][slot]
+        for i, k, off, nb, dt, shp in ent["items"]:
+            st[off:off + nb].view(dt).view(shp).copy_(mbs[i][k])
+        st[ent["steps_off"]:ent["steps_off"] + 8 * n].view(torch.int64).copy_(
+            torch.arange(model.micro_step + 1, model.micro_step + n + 1, dtype=torch.int64))
+        st[ent["inv_off"]:ent["inv_off"] + 4].view(torch.float32).fill_(1.0 / float(ntok))
+        ent["dbuf"].copy_(st, non_blocking=True)
+        if ent["stage_ev"][slot] is None:
+            ent["stage_ev"][slot] = torch.cuda.Event()
+        ent["stage_ev"][slot].record()
         ent["graph"].replay()
         model.micro_step += n
         return ent["loss"]
