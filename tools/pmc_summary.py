@@ -51,7 +51,7 @@ def main():
         avg = tot / n
         wc = c.get("SQ_WAVE_CYCLES", 0.0)
         f = lambda name: (100.0 * c[name] / wc) if wc and name in c else float("nan")
-        mfma = 100.0 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (tot * CLK_GHZ * SIMDS) * 2 if "SQ_VALU_MFMA_BUSY_CYCLES" in c else float("nan")
+        mfma = 100.0 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (tot * CLK_GHZ * SIMDS) if "SQ_VALU_MFMA_BUSY_CYCLES" in c else float("nan")
         hbm = (2 * c["FETCH_SIZE"] * 1024 / (tot * 1e-9) / 1e9) / 2 if "FETCH_SIZE" in c else float("nan")
         lds = c.get("SQ_LDS_BANK_CONFLICT", float("nan")) / (n / 2)
         print(f"{tot/1e3:9.1f} {n:5d} {avg/1e3:8.1f} {mfma:6.1f} {f('SQ_WAIT_ANY'):6.1f} {f('SQ_WAIT_INST_ANY'):6.1f} "
