@@ -141,3 +141,52 @@ def test_opt_arena_multi_adapter_matches_dense():
     fused2(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
     arena.rebind_grads()
     _grad_close(fused, fused2, 2e-2)
+
+
+def test_fused_backward_notifies_dp_reducer_per_layer(monkeypatch):
+    """DDP overlap on the fused path (mift.ops.fused._notify -> arena.grad_ready, which the DP
+    reducer turns into bucket all-reduces): a fake reducer records the order of notifications
+    against the dgrad GEMMs.  Layer l's adapters must be reported final BEFORE layer l-1's dgrad
+    GEMMs are queued — otherwise no all-reduce could overlap the rest of backward (VERDICT r2 #8)."""
+    import re
+    from mift.lora import LoraArena
+    from mift.lora.pack import attach
+    from mift.ops import fused as F
+    cfg = GPT2Config(vocab_size=1000, n_positions=128, n_embd=128, n_layer=4, n_head=2, n_inner=512,
+                     embd_pdrop=0.0, attn_pdrop=0.0, resid_pdrop=0.0)
+    model = GPT2LMHeadModel(cfg, dtype=torch.bfloat16, device="cuda").init_weights(3)
+    L.inject(model, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.0, target_modules=["c_attn", "c_proj"]))
+    arena = LoraArena(model)
+    attach(model, arena, torch.bfloat16)
+    layer_of = {}
+    for (n, _), off in zip(arena.named, arena.offsets):
+        layer_of[off] = int(re.search(r"\.h\.(\d+)\.", n).group(1))
+    events = []
+    arena.grad_ready = lambda offs: events.append(("notify", {layer_of[o] for o in offs}))
+    real_gemm = F.K.gemm
+
+    def gemm(*a, **k):
+        events.append(("gemm", None))
+        return real_gemm(*a, **k)
+
+    monkeypatch.setattr(F.K, "gemm", gemm)
+    model.train()
+    ids = torch.randint(0, cfg.vocab_size, (4, 64), device="cuda")
+    loss = model(input_ids=ids, labels=ids, reduction="sum")["loss"]
+    events.clear()  # forward GEMMs are not of interest
+    loss.backward()
+    torch.cuda.synchronize()
+    notes = [(i, ls) for i, (kind, ls) in enumerate(events) if kind == "notify"]
+    seen = set().union(*[ls for _, ls in notes])
+    assert seen == set(range(cfg.n_layer)), seen
+    order = [max(ls) for _, ls in notes]
+    assert order == sorted(order, reverse=True), order  # last layer first
+    last_of = {}
+    for i, ls in notes:
+        for l in ls:
+            last_of[l] = i
+    for l in range(cfg.n_layer - 1, 0, -1):
+        # a dgrad GEMM of an earlier layer runs AFTER layer l's final notification
+        assert any(kind == "gemm" for kind, _ in events[last_of[l] + 1:]), (l, events)
+    # and the arena grads are the real ones (non-zero)
+    assert arena.grad.abs().sum().item() > 0

@@ -308,6 +308,51 @@ def test_lora_wgrad_group(dt):
     assert arena[~covered].abs().max().item() == 0.0  # nothing written outside the slots
 
 
+@pytest.mark.parametrize("det", ["1", "0"])
+def test_lora_wgrad_group_deterministic(det, monkeypatch):
+    """Deterministic mode (default): slab partials + ordered reduction, so repeated launches on the
+    same inputs give ONE bit pattern; MIFT_DETERMINISTIC=0 (fp32 atomics) stays
+    numerically correct."""
+    monkeypatch.setenv("MIFT_DETERMINISTIC", det)
+    C = _C()
+    torch.manual_seed(5)
+    M, K = 8192, 3072  # distilgpt2 mlp.c_proj dA: many row chunks per column tile
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    dT = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
+    meta = [2, 1, 0, 8, 64] + [0, 0, 0] * 3 + [9]
+    outs = []
+    for _ in range(5 if det == "1" else 1):
+        arena = torch.full((64 + 8 * K + 64,), 0.25, device="cuda")  # accumulates onto existing grads
+        C.lora_wgrad_group(arena, [x], [dT], meta, [0.05])
+        outs.append(arena)
+    exp = (ref.dropout(x.float(), 0.05, 9).t() @ dT.float()[:, :8]).t().reshape(-1) + 0.25
+    got = outs[0][64:64 + 8 * K]
+    assert ((got - exp).norm() / exp.norm()).item() < 1e-2
+    assert outs[0][:64].eq(0.25).all() and outs[0][64 + 8 * K:].eq(0.25).all()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), "deterministic wgrad must be bit-reproducible"
+
+
+def test_grad_stats_deterministic():
+    """grad_stats run 100x on the same arena gives one bit pattern (per-block partials + one
+    fixed-order reduction block, no float atomics), close to the fp64 sum; non-finite count exact."""
+    C = _C()
+    g = torch.randn(11_796_481, device="cuda") * 1e-3  # OPT-2.7B LoRA arena size (+1: ragged tail)
+    stats = torch.zeros(2, device="cuda")
+    ref_s = (g.double() ** 2).sum().item()
+    seen = set()
+    for _ in range(100):
+        C.grad_stats(g, stats)
+        seen.add(tuple(stats.cpu().view(torch.int32).tolist()))
+    assert len(seen) == 1, seen
+    assert stats[0].item() == pytest.approx(ref_s, rel=1e-5)
+    assert stats[1].item() == 0.0
+    g[12345] = float("inf")
+    g[-1] = float("nan")
+    C.grad_stats(g, stats)
+    assert stats[1].item() == 2.0
+
+
 @pytest.mark.parametrize("rank,D", [(8, 768), (28, 2560), (16, 1024)])
 @pytest.mark.parametrize("p", [0.0, 0.05])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])

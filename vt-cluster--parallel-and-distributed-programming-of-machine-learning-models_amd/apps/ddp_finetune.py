@@ -85,6 +85,23 @@ def load_data(args, tok_vocab_pad, rank):
     return ("text", read_text_lines(data_file), data_file)
 
 
+def _write_job_meta(args, world, ctx):
+    """``{logdir}/meta.json`` (reference P1 sbatch :72-87) unless the launcher already wrote one, so
+    ``summarize_medium_times.py`` reports N and the dataset for app-only runs too."""
+    path = os.path.join(args.logdir, "meta.json")
+    if os.path.exists(path):
+        return
+    os.makedirs(args.logdir, exist_ok=True)
+    meta = {"job_id": os.environ.get("SLURM_JOB_ID", os.path.basename(os.path.abspath(args.logdir))),
+            "nnodes": int(os.environ.get("SLURM_NNODES", "1")), "world_size": world,
+            "n_gpus": world if ctx.device.type == "cuda" else 0, "dataset": args.dataset,
+            "data_file": args.data_file or DATASETS[args.dataset], "seq_len": args.seq_len, "epochs": args.epochs,
+            "batch": args.batch, "accum": args.accum, "lr": args.lr, "model": args.model,
+            "start": datetime.datetime.now().isoformat(timespec="seconds")}
+    with open(path, "w") as f:
+        json.dump(meta, f, indent=2)
+
+
 def main(argv=None, defaults=None):
     args = build_argparser(defaults).parse_args(argv)
     torch.manual_seed(args.seed)
@@ -102,6 +119,8 @@ def main(argv=None, defaults=None):
     if not gpu and dtype != torch.float32:
         dtype = torch.float32  # CPU path keeps fp32 weights (autocast bf16 optional)
     logs = PhaseLogger(args.logdir, rank)
+    if rank == 0:
+        _write_job_meta(args, world, ctx)
 
     # --- Dataset load ---
     t0 = time.perf_counter()

@@ -12,6 +12,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define MIFT_HD __device__ __forceinline__
 
@@ -47,6 +48,13 @@ __device__ __forceinline__ uint64_t mift_seed(uint64_t s, const int64_t* sstep) 
 }
 // host: the device micro-step counter bound by mift._C.set_seed_step (nullptr = eager)
 const int64_t* mift_seed_step();
+
+// host: deterministic reductions — no float atomics in any gradient reduction, so a
+// step's results are bit-identical run to run.  On by default; MIFT_DETERMINISTIC=0 opts out.
+inline bool mift_deterministic() {
+  const char* e = getenv("MIFT_DETERMINISTIC");
+  return e == nullptr || e[0] != '0';
+}
 
 typedef __bf16 bf16;
 typedef _Float16 fp16;

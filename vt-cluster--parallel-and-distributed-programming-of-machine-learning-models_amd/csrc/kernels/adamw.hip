@@ -1,10 +1,12 @@
 // K9: fused optimizer step over the flat LoRA arena (mift.lora.LoraArena).
 //
-// Three launches, everything stays on the device (no host sync, capturable
-// into a hipGraph):
-//   1. grad_stats:  sum(g^2) and a non-finite flag over the arena, written to
-//                   stats[0..1] (fp32).  For PP / ZeRO-1 the caller all-reduces
-//                   `stats` over the model-parallel group between 1 and 2.
+// Launches, everything stays on the device (no host sync, capturable into a hipGraph):
+//   1. grad_stats:  per-block partial sum(g^2) and non-finite counts of the arena, then ONE block
+//                   sums the partials in a fixed order into stats[0..1] (fp32).  No float atomics:
+//                   the result is bit-identical run to run, so DDP replicas that hold identical
+//                   all-reduced grads derive identical clip coefficients (SURVEY §5.2 deterministic
+//                   mode).  For PP / ZeRO-1 the caller all-reduces `stats` over
+//                   the model-parallel group between 1 and 2.
 //   2. opt_finalize (1 thread): unscale (fp16 loss scaling), global-norm clip
 //                   coefficient (max_norm, reference clip 1.0), found_inf,
 //                   step += !found_inf, dynamic loss-scale update.
@@ -19,8 +21,10 @@
 
 namespace {
 
+// Pass 1: block b writes (sum g^2, non-finite count) of its grid-strided elements to part[b].
+// The element -> thread assignment and the block reduction tree are fixed, so each partial is too.
 __global__ __launch_bounds__(256) void grad_stats_kernel(const float* __restrict__ g, int64_t n,
-                                                         float* __restrict__ stats) {
+                                                         float2* __restrict__ part) {
   __shared__ float red[4];
   float s = 0.f;
   float bad = 0.f;
@@ -29,20 +33,37 @@ __global__ __launch_bounds__(256) void grad_stats_kernel(const float* __restrict
     if (i + 3 < n) {
       float4 v = *reinterpret_cast<const float4*>(g + i);
       s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-      if (!isfinite(v.x) || !isfinite(v.y) || !isfinite(v.z) || !isfinite(v.w)) bad = 1.f;
+      if (!isfinite(v.x) || !isfinite(v.y) || !isfinite(v.z) || !isfinite(v.w)) bad += 1.f;
     } else {
       for (int64_t j = i; j < n; ++j) {
         s += g[j] * g[j];
-        if (!isfinite(g[j])) bad = 1.f;
+        if (!isfinite(g[j])) bad += 1.f;
       }
     }
   }
   s = block_sum<4>(s, red);
   __syncthreads();
   bad = block_sum<4>(bad, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = make_float2(s, bad);
+}
+
+// Pass 2 (one block): thread t sums partials t, t + 256, ... in index order, then the fixed block
+// tree — the same bits for the same gradients on every run and every replica.
+__global__ __launch_bounds__(256) void grad_stats_reduce_kernel(const float2* __restrict__ part, int np,
+                                                                float* __restrict__ stats) {
+  __shared__ float red[4];
+  float s = 0.f, bad = 0.f;
+  for (int i = threadIdx.x; i < np; i += 256) {
+    const float2 v = part[i];
+    s += v.x;
+    bad += v.y;
+  }
+  s = block_sum<4>(s, red);
+  __syncthreads();
+  bad = block_sum<4>(bad, red);
   if (threadIdx.x == 0) {
-    atomicAdd(stats, s);
-    if (bad > 0.f) atomicAdd(stats + 1, 1.f);
+    stats[0] = s;
+    stats[1] = bad;
   }
 }
 
@@ -135,9 +156,13 @@ int grid_for(int64_t n) {
 
 void mift_grad_stats(const at::Tensor& g, at::Tensor& stats) {
   TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.is_contiguous(), "grad_stats: fp32 contiguous");
+  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kFloat && stats.numel() >= 2, "grad_stats: stats[2]");
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-  stats.zero_();
-  grad_stats_kernel<<<grid_for(g.numel()), 256, 0, st>>>(g.data_ptr<float>(), g.numel(), stats.data_ptr<float>());
+  const int nb = grid_for(g.numel());
+  auto part = at::empty({2 * (int64_t)nb}, g.options());
+  grad_stats_kernel<<<nb, 256, 0, st>>>(g.data_ptr<float>(), g.numel(), reinterpret_cast<float2*>(part.data_ptr<float>()));
+  grad_stats_reduce_kernel<<<1, 256, 0, st>>>(reinterpret_cast<const float2*>(part.data_ptr<float>()), nb,
+                                              stats.data_ptr<float>());
 }
 
 void mift_opt_finalize(const at::Tensor& stats, at::Tensor& state, double max_norm, bool dynamic_scale,

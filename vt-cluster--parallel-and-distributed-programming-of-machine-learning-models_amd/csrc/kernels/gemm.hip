@@ -18,7 +18,9 @@
 // owns (BM/NWM) x (BN/NWN) as 16x16 MFMA tiles (mfma_f32_16x16x32).
 // Global->LDS staging by global_load_lds_dwordx4 (no VGPR round trip) into
 // an NSTAGE-deep ring of XOR-swizzled images (16-B chunk c of row r stored at
-// chunk c ^ (r & 7): every ds_read_b128 fragment read is conflict-free;
+// chunk c ^ (r & 7): the ds_read_b128 fragment reads of rows r0..r0+15 (r0 % 8 == 0) cover all 16
+// slots of a 256-B bank row per 16-lane group, i.e. conflict-free by the §LDS bank rule — the PMC
+// conflicts of round 2 came from the epilogue's C-tile image, see CTile below);
 // swizzle applied on the per-lane global SOURCE address because the LDS-DMA
 // destination is lane-linear, guide rule 21).  NSTAGE-1 tiles are in flight:
 // each K step waits with a COUNTED s_waitcnt vmcnt (never 0 in steady state)
@@ -171,6 +173,42 @@ MIFT_HD void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+
+// ---- C-tile staging image in LDS (epilogue phase 1 -> phase 2) ----
+// Unit = 8 bytes (4 16-bit elements).  Row r's unit u is stored at unit u ^ sw(r) of a row of CLDU
+// units.  Phase 1 writes one unit per lane (ds_write_b64: 16-lane groups, bank = dword % 32; the
+// 16 lanes of a group hold rows r0..r0+15 of ONE logical unit); phase 2 reads 16 B = units
+// (2k, 2k+1) per lane (ds_read_b128, bank = dword % 64), which the XOR keeps adjacent (swapped
+// when sw(r) is odd).  BN % 64 == 0: CLDU = BN/4 (whole 128-B bank rows) and sw(r) = r & 15 —
+// conflict-free for both phases.  BN = 96 (12 chunks per row, so a phase-2 lane group straddles
+// rows): CLDU = 40 and a 32-row permutation table found by an exhaustive bank model of both phases
+// (lane groups per MI355X_MICROARCH.md §LDS; the model reproduces the PMC count of the plain
+// layout exactly, 192 conflict cycles per block) -> 0 on writes, 32 cycles per block on reads.
+// The round-2 BN+8 padding was 2-way on every phase-1 write (PMC: 1.08 M conflict cycles per
+// 128x192 dispatch, 12.9 M per LM-head forward).
+template <int BN>
+struct CTile {
+  static constexpr int CLDU = BN % 64 == 0 ? BN / 4 : 40;
+  static constexpr int CLD = CLDU * 4;  // elements
+  static_assert(BN % 64 == 0 || BN == 96, "C-tile swizzle: BN % 64 == 0 or BN == 96");
+  static MIFT_HD int sw(int row) {
+    if constexpr (BN % 64 == 0) {
+      return row & 15;
+    } else {
+      const uint64_t t = (row & 16) ? 0xe8fb5163d9ac2074ull : 0xdcfa34028eb97156ull;
+      return (int)((t >> ((row & 15) * 4)) & 15);
+    }
+  }
+  // element offset of the 4 elements at (row, col), col % 4 == 0
+  static MIFT_HD int off4(int row, int col) { return row * CLD + (((col >> 2) ^ sw(row)) << 2); }
+  // the 8 elements at (row, c8), c8 % 8 == 0
+  static MIFT_HD short8 read8(const void* cs, int row, int c8) {
+    const int x = sw(row);
+    const short8 v = *reinterpret_cast<const short8*>(reinterpret_cast<const short*>(cs) + row * CLD +
+                                                       ((((c8 >> 2) ^ x) & ~1) << 2));
+    return (x & 1) ? short8{v[4], v[5], v[6], v[7], v[0], v[1], v[2], v[3]} : v;
+  }
+};
 
 template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, bool SKM, int EPI = 0>
 __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
@@ -426,7 +464,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     // ---- epilogue phase 1: accumulators -> LDS tile (one 8-byte write per 16x16 tile) ----
     __syncthreads();  // staging ring is reused for the C tile
     T* Cs = reinterpret_cast<T*>(smem);
-    constexpr int CLD = BN + 8;
+    using CT = CTile<BN>;
     const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
   #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -453,7 +491,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   #pragma unroll
           for (int e = 0; e < 4; ++e) z[e] += kp[e] ? xt[e] * ep.ext_inv_keep : 0.f;
         }
-        store4<T>(Cs + row * CLD + col, z);
+        store4<T>(Cs + CT::off4(row, col), z);
       }
     }
     __syncthreads();
@@ -489,7 +527,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       const int gr = m0 + row, gc = n0 + c8;
       if (gr >= M || gc >= N) return;
       float z[8];
-      load8<T>(Cs + row * CLD + c8, z);
+      unpack8<T>(CT::read8(Cs, row, c8), z);
       const size_t off = (size_t)gr * ldc + gc;
       const bool full = gc + 8 <= N;
       if (ep.pre_add != nullptr) {
@@ -574,7 +612,8 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   // waves' partials of a row.
   auto lm_fwd_epilogue = [&]() {
     const LmArgs& lm = ep.lm;
-    constexpr int CLD = BN + 8;
+    using CT = CTile<BN>;
+    constexpr int CLD = CT::CLD;
     __syncthreads();  // every wave is done reading the staging ring
     T* Cs = reinterpret_cast<T*>(smem);
     float* redm = reinterpret_cast<float*>(smem + BM * CLD * sizeof(T));
@@ -631,7 +670,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
           const float4_ a = acc[i][j];
           lm.zlab[row] = d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
         }
-        store4<T>(Cs + lrow * CLD + lcol, ev);
+        store4<T>(Cs + CT::off4(lrow, lcol), ev);
       }
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
@@ -659,7 +698,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       const int r = v / VPR, c8 = (v % VPR) * 8;
       const int gr = m0 + r, gc = n0 + c8;
       if (gr < M && gc < N)
-        *reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc) = *reinterpret_cast<const short8*>(Cs + r * CLD + c8);
+        *reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc) = CT::read8(Cs, r, c8);
     }
   };
 
@@ -721,10 +760,13 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     for (int w0 = g0; w0 < g1; w0 += LM_GW) {
       const int w1 = min(g1, w0 + LM_GW), nw = w1 - w0;
       __syncthreads();  // the previous window's readers are done
-      for (int x = tid; x < BM * nw; x += NT) {
-        const int r = x / nw, g = x % nw;
-        const int row = min(m0 + r, M - 1);
-        ms[r * cstride + g] = lm.stats[(size_t)row * lm.ntn + w0 + g].x;
+      // one 32-lane half-wave per row (nw <= 32 lanes active): each half writes one row's nw words
+      // -> distinct banks (ds_write_b32 groups are the two half-waves), and reads a contiguous run
+      // of the row's stats from global; the odd stride keeps the fragment-row reads conflict-free
+      static_assert(LM_GW <= 32, "window fill: one half-wave per row");
+      for (int r = tid >> 5; r < BM; r += NT / 32) {
+        const int g = tid & 31;
+        if (g < nw) ms[r * cstride + g] = lm.stats[(size_t)min(m0 + r, M - 1) * lm.ntn + w0 + g].x;
       }
       __syncthreads();
       mainloop8(w0 * GK, min(nk_all, w1 * GK), [&](int kt) {
@@ -864,7 +906,7 @@ template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                  int K, const EpiArgs& ep, hipStream_t st) {
   constexpr int STAGE_BYTES = (BM + BN) * ROWB;
-  constexpr int EPI_BYTES = BM * (BN + 8) * 2;
+  constexpr int EPI_BYTES = BM * CTile<BN>::CLD * 2;
   constexpr int RING = (NSTAGE == 0 ? 2 : NSTAGE) * STAGE_BYTES;
   constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
   constexpr int NT = NWM * NWN * 64;
@@ -1062,7 +1104,7 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   }
   SkArgs sk{};
   // staging ring (128 KiB) reused for the E tile + the two row-partial arrays
-  constexpr int SMEM = std::max(2 * (BM + BN) * ROWB, BM * (BN + 8) * 2 + 2 * 8 * (BM / 2) * 4 + BM * 4);
+  constexpr int SMEM = std::max(2 * (BM + BN) * ROWB, BM * CTile<BN>::CLD * 2 + 2 * 8 * (BM / 2) * 4 + BM * 4);
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>;
   static bool attr = false;

@@ -127,13 +127,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         sg += g[it][i];
         sgx += g[it][i] * xh[it][i];
       }
-      if (dw != nullptr) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          atomicAdd(dw + c + i, dv[i] * xh[it][i]);
-          atomicAdd(db + c + i, dv[i]);
-        }
-      }
     }
   }
   sg = wave_sum(sg) / D;
@@ -164,6 +157,42 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
   }
+}
+
+// dgamma / dbeta (trainable LayerNorm, e.g. full fine-tuning), deterministic: pass 1 sums a chunk
+// of LN_WG_ROWS rows per (column, chunk) in row order, pass 2 sums the chunks in order — no
+// float atomics.
+constexpr int LN_WG_ROWS = 128;
+template <typename T>
+__global__ __launch_bounds__(256) void ln_wgrad_partial_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd, float* __restrict__ pw,
+                                                               float* __restrict__ pb, int M, int D) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= D) return;
+  const int r0 = blockIdx.y * LN_WG_ROWS, r1 = min(M, r0 + LN_WG_ROWS);
+  float sw = 0.f, sb = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const float g = (float)dy[(size_t)r * D + c];
+    sw += g * ((float)x[(size_t)r * D + c] - mean[r]) * rstd[r];
+    sb += g;
+  }
+  pw[(size_t)blockIdx.y * D + c] = sw;
+  pb[(size_t)blockIdx.y * D + c] = sb;
+}
+
+__global__ __launch_bounds__(256) void ln_wgrad_reduce_kernel(const float* __restrict__ pw, const float* __restrict__ pb,
+                                                              float* __restrict__ dw, float* __restrict__ db, int nch,
+                                                              int D) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= D) return;
+  float sw = 0.f, sb = 0.f;
+  for (int k = 0; k < nch; ++k) {
+    sw += pw[(size_t)k * D + c];
+    sb += pb[(size_t)k * D + c];
+  }
+  dw[c] = sw;
+  db[c] = sb;
 }
 
 template <typename T, typename W, int N>
@@ -263,16 +292,37 @@ std::vector<at::Tensor> mift_layer_norm_bwd(const at::Tensor& dy, const at::Tens
   auto dx = at::empty_like(x);
   c10::optional<at::Tensor> dbranch, dw, db;
   if (want_branch) dbranch = at::empty_like(x);
-  if (want_wgrad) {
-    dw = at::zeros({D}, x.options().dtype(at::kFloat));
-    db = at::zeros({D}, x.options().dtype(at::kFloat));
-  }
   uint32_t thr = mift_thr16(p);
   float inv_keep = p > 0 ? mift_inv_keep(p) : 1.f;
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  const c10::optional<at::Tensor> none;
   DISPATCH_TW(x.scalar_type(), w.scalar_type(),
-              launch_bwd<T, W>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, (uint64_t)seed, thr,
+              launch_bwd<T, W>(dy, x, w, mean, rstd, dres, dx, dbranch, none, none, M, D, (uint64_t)seed, thr,
                                inv_keep, st));
+  if (want_wgrad) {
+    dw = at::empty({D}, x.options().dtype(at::kFloat));
+    db = at::empty({D}, x.options().dtype(at::kFloat));
+    const int nch = std::max(1, (M + LN_WG_ROWS - 1) / LN_WG_ROWS);
+    auto part = at::empty({2, (int64_t)nch, D}, x.options().dtype(at::kFloat));
+    float* pw = part.data_ptr<float>();
+    float* pb = pw + (size_t)nch * D;
+    const dim3 g1((D + 255) / 256, nch);
+    if (M > 0) {
+      if (x.scalar_type() == at::kBFloat16)
+        ln_wgrad_partial_kernel<bf16><<<g1, 256, 0, st>>>((const bf16*)dy.data_ptr(), (const bf16*)x.data_ptr(),
+                                                          mean.data_ptr<float>(), rstd.data_ptr<float>(), pw, pb, M, D);
+      else if (x.scalar_type() == at::kHalf)
+        ln_wgrad_partial_kernel<fp16><<<g1, 256, 0, st>>>((const fp16*)dy.data_ptr(), (const fp16*)x.data_ptr(),
+                                                          mean.data_ptr<float>(), rstd.data_ptr<float>(), pw, pb, M, D);
+      else
+        ln_wgrad_partial_kernel<float><<<g1, 256, 0, st>>>(dy.data_ptr<float>(), x.data_ptr<float>(),
+                                                           mean.data_ptr<float>(), rstd.data_ptr<float>(), pw, pb, M, D);
+      ln_wgrad_reduce_kernel<<<(D + 255) / 256, 256, 0, st>>>(pw, pb, dw->data_ptr<float>(), db->data_ptr<float>(), nch, D);
+    } else {
+      dw->zero_();
+      db->zero_();
+    }
+  }
   std::vector<at::Tensor> out{dx};
   out.push_back(want_branch ? *dbranch : at::Tensor());
   out.push_back(want_wgrad ? *dw : at::Tensor());

@@ -16,12 +16,17 @@
 //     ds_read_b64_tr_b16 (guide T10).  Rows are consumed in a permuted order
 //     (group g takes rows 4g..4g+3 and 16+4g..16+4g+3 of each 32-row step) so a
 //     half-wave's 8 rows sit at an odd multiple of 32 B apart -> conflict-free.
-//     Split over M across blocks, fp32 atomics into the small [P,32] output.
+//     Split over M across blocks.  Deterministic (default, MIFT_DETERMINISTIC != 0): every block
+//     stores its fp32 partial tile to a slab and lora_wgrad_reduce adds the row-chunk partials of a
+//     column tile in chunk order into the output (bit-identical run to run); with
+//     MIFT_DETERMINISTIC=0 the blocks add into the output with fp32 atomics instead.
 #include "common.h"
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include <algorithm>
 #include <tuple>
+#include <vector>
 
 namespace {
 
@@ -210,6 +215,7 @@ struct WgProb {
   const void* X;    // [M, P] rows of stride ldx (a column slice of a wider tensor is fine)
   const void* Y;    // [M, 32] contiguous
   int ldx, P, M, rows, blk0, mode, nslot;
+  int tile0;        // first column tile of this problem in the reduction launch (deterministic mode)
   uint32_t thr;     // LoRA-input dropout on X (dA): keep iff hash >= thr, index = row * P + col
   float inv_keep;
   uint64_t seed;
@@ -217,10 +223,44 @@ struct WgProb {
 };
 struct WgArgs {
   float* out;
+  float* ws;        // deterministic mode: [blocks][NQT*16][64] fp32 partial slabs (nullptr: atomics)
   const int64_t* sstep;
   int np;
   WgProb p[WG_MAXP];
 };
+
+// Output index of element (pp, q) of problem pr's [P, 32] product (-1: column q feeds no slot).
+// mode 0: dense [P,32] at slot 0; mode 1: dB [P, rank]; mode 2: dA [rank, P] per slot.
+MIFT_HD int64_t wg_out_index(const WgProb& pr, int64_t pp, int q, int si) {
+  if (pr.mode == 0) return si == 0 ? pr.slot[0].offset + pp * 32 + q : -1;
+  const WgSlot& sl = pr.slot[si];
+  if (q < sl.qoff || q >= sl.qoff + sl.rank) return -1;
+  return sl.offset + (pr.mode == 1 ? pp * sl.rank + (q - sl.qoff) : (int64_t)(q - sl.qoff) * pr.P + pp);
+}
+
+// Block epilogue of both wgrad kernels: acc[c][r] = product[p0 + wave*16 + g*4 + r][c*16 + li].
+template <int NQT>
+MIFT_HD void wg_store(const WgArgs& args, const WgProb& pr, const float4_ (&acc)[NQT], int p0, int wave, int g, int li) {
+  if (args.ws != nullptr) {  // deterministic: slab [c][li][64 rows of p], one 16-B store per (c)
+    float* slab = args.ws + (size_t)blockIdx.x * (NQT * 16 * 64);
+#pragma unroll
+    for (int c = 0; c < NQT; ++c)
+      *reinterpret_cast<float4_*>(slab + (c * 16 + li) * 64 + wave * 16 + g * 4) = acc[c];
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < NQT; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t pp = p0 + wave * 16 + g * 4 + r;
+      const int q = c * 16 + li;
+#pragma unroll 1
+      for (int si = 0; si < (pr.mode == 0 ? 1 : pr.nslot); ++si) {
+        const int64_t o = wg_out_index(pr, pp, q, si);
+        if (o >= 0) atomicAdd(args.out + o, acc[c][r]);
+      }
+    }
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void lora_wgrad_kernel(const WgArgs args) {
@@ -332,27 +372,7 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const WgArgs args) {
       acc[1] = mfma16<T>(af, bf1, acc[1]);
     }
   }
-  // acc[c][r] = out[p = p0 + wave*16 + g*4 + r][q = c*16 + li]
-  // mode 0: dense [P,32] at out + slot[0].offset; mode 1: dB [P, rank]; mode 2: dA [rank, P] per slot
-  float* out = args.out;
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t pp = p0 + wave * 16 + g * 4 + r;
-      const int q = c * 16 + li;
-      if (pr.mode == 0) {
-        atomicAdd(out + pr.slot[0].offset + pp * 32 + q, acc[c][r]);
-        continue;
-      }
-#pragma unroll 1
-      for (int si = 0; si < pr.nslot; ++si) {
-        const WgSlot& sl = pr.slot[si];
-        if (q >= sl.qoff && q < sl.qoff + sl.rank)
-          atomicAdd(out + sl.offset + (pr.mode == 1 ? pp * sl.rank + (q - sl.qoff) : (int64_t)(q - sl.qoff) * P + pp),
-                    acc[c][r]);
-      }
-    }
+  wg_store<2>(args, pr, acc, p0, wave, g, li);
 }
 
 // v2 (default; MIFT_WGRAD_V=1 selects the kernel above): the same tiles and LDS images, but two
@@ -485,25 +505,41 @@ __global__ __launch_bounds__(256) void lora_wgrad2_kernel(const WgArgs args) {
 #pragma unroll
     for (int c = 0; c < NQT; ++c) acc[c] *= inv_keep;
   }
-  float* out = args.out;
+  wg_store<NQT>(args, pr, acc, p0, wave, g, li);
+}
+
+// Deterministic reduction: block t = column tile t of the launch (problem pi, tile pt) sums the
+// row-chunk slabs of that tile in chunk order and adds the result to the output — each output
+// element is owned by exactly one thread (the host checks that the problems' slots are disjoint).
+template <int NQT>
+__global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const WgArgs args) {
+  int pi = 0;
+#pragma unroll 1
+  while (pi + 1 < args.np && (int)blockIdx.x >= args.p[pi + 1].tile0) ++pi;
+  const WgProb& pr = args.p[pi];
+  const int ntp = pr.P / 64;
+  const int pt = blockIdx.x - pr.tile0;
+  const int nch = (pr.M + pr.rows - 1) / pr.rows;
+  constexpr int SL = NQT * 16 * 64;
 #pragma unroll
-  for (int c = 0; c < NQT; ++c)
+  for (int k = 0; k < NQT; ++k) {
+    const int e = (threadIdx.x + 256 * k) * 4;  // slab element: [c][li][p]
+    const int c = e / 1024, li = (e / 64) % 16, pl = e % 64;
+    float4_ sum = float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int ch = 0; ch < nch; ++ch)
+      sum += *reinterpret_cast<const float4_*>(args.ws + (size_t)(pr.blk0 + ch * ntp + pt) * SL + e);
+    const int q = c * 16 + li;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t pp = p0 + wave * 16 + g * 4 + r;
-      const int q = c * 16 + li;
-      if (pr.mode == 0) {
-        atomicAdd(out + pr.slot[0].offset + pp * 32 + q, acc[c][r]);
-        continue;
-      }
+      const int64_t pp = (int64_t)pt * 64 + pl + r;
 #pragma unroll 1
-      for (int si = 0; si < pr.nslot; ++si) {
-        const WgSlot& sl = pr.slot[si];
-        if (q >= sl.qoff && q < sl.qoff + sl.rank)
-          atomicAdd(out + sl.offset + (pr.mode == 1 ? pp * sl.rank + (q - sl.qoff) : (int64_t)(q - sl.qoff) * P + pp),
-                    acc[c][r]);
+      for (int si = 0; si < (pr.mode == 0 ? 1 : pr.nslot); ++si) {
+        const int64_t o = wg_out_index(pr, pp, q, si);
+        if (o >= 0) args.out[o] += sum[r];
       }
     }
+  }
 }
 
 }  // namespace
@@ -586,18 +622,34 @@ void launch_wgrad(WgArgs& args, hipStream_t st) {
     blk += (p.P / 64) * ((p.M + p.rows - 1) / p.rows);
   }
   if (blk == 0) return;
-  const char* ve = getenv("MIFT_WGRAD_V");  // A/B knob, read per launch: 1 = the v1 kernel
-  if (ve != nullptr && atoi(ve) == 1) {
-    lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
-    return;
-  }
   bool narrow = true;  // every slot within columns [0, 16)
   for (int i = 0; i < args.np; ++i) {
     if (args.p[i].mode == 0) narrow = false;
     for (int si = 0; si < args.p[i].nslot; ++si)
       if (args.p[i].slot[si].qoff + args.p[i].slot[si].rank > 16) narrow = false;
   }
-  if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
+  const char* ve = getenv("MIFT_WGRAD_V");  // A/B knob, read per launch: 1 = the v1 kernel
+  const bool v1 = ve != nullptr && atoi(ve) == 1;
+  const int nqt = (narrow && !v1) ? 1 : 2;
+  at::Tensor ws;
+  if (mift_deterministic()) {
+    ws = at::empty({(int64_t)blk * nqt * 16 * 64}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
+    args.ws = ws.data_ptr<float>();
+    int tiles = 0;
+    for (int i = 0; i < args.np; ++i) {
+      args.p[i].tile0 = tiles;
+      tiles += args.p[i].P / 64;
+    }
+    if (v1) lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
+    else if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
+    else lora_wgrad2_kernel<T, 2><<<blk, 256, 0, st>>>(args);
+    if (nqt == 1) lora_wgrad_reduce_kernel<1><<<tiles, 256, 0, st>>>(args);
+    else lora_wgrad_reduce_kernel<2><<<tiles, 256, 0, st>>>(args);
+    return;
+  }
+  args.ws = nullptr;
+  if (v1) lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
+  else if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
   else lora_wgrad2_kernel<T, 2><<<blk, 256, 0, st>>>(args);
 }
 }  // namespace
@@ -654,6 +706,17 @@ void mift_lora_wgrad_group(at::Tensor& out, const std::vector<at::Tensor>& xs, c
   }
   args.np = n;
   if (n == 0) return;
+  if (mift_deterministic()) {  // the reduction kernel writes each output element from ONE thread
+    std::vector<std::pair<int64_t, int64_t>> iv;
+    for (int i = 0; i < n; ++i)
+      for (int si = 0; si < (args.p[i].mode == 0 ? 1 : args.p[i].nslot); ++si) {
+        const WgSlot& sl = args.p[i].slot[si];
+        iv.emplace_back(sl.offset, sl.offset + (int64_t)args.p[i].P * (args.p[i].mode == 0 ? 32 : sl.rank));
+      }
+    std::sort(iv.begin(), iv.end());
+    for (size_t k = 1; k < iv.size(); ++k)
+      TORCH_CHECK(iv[k].first >= iv[k - 1].second, "lora_wgrad_group: overlapping output slots in one launch");
+  }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   if (dt == at::kBFloat16) launch_wgrad<bf16>(args, st);
   else launch_wgrad<fp16>(args, st);

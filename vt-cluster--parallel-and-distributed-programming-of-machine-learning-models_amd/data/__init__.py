@@ -231,6 +231,19 @@ class MicroBatcher:
         n = len(self.indices(0))
         return (n + self.mb * self.accum - 1) // (self.mb * self.accum)
 
+    def sample_step(self):
+        """One full-shape optimizer step (``accum`` micro-batches of ``mb`` rows) built from the first
+        rows of the dataset, without touching the epoch iterators — the Trainer's setup-time warm-up
+        and graph capture use its shapes; its values never reach the model's parameters."""
+        n = min(self.mb, len(self.ds))
+        b = self.ds.batch(np.arange(n))
+        if n < self.mb:  # tiny datasets: repeat rows to the full micro-batch shape
+            rep = (self.mb + n - 1) // n
+            b = {k: v.repeat(rep, 1)[:self.mb] for k, v in b.items()}
+        step = StepBatch(dict(b) for _ in range(self.accum))
+        step.global_tokens = None
+        return step
+
     def micro_batches_per_epoch(self):
         n = len(self.indices(0))
         return (n + self.mb - 1) // self.mb

@@ -191,7 +191,8 @@ def summarize_times(logdirs, title):
     out = [title, "-" * 70]
     for ld in logdirs:
         meta, t, wall = read_meta(ld), training_seconds(ld), read_wall(ld)
-        n = meta.get("nnodes", meta.get("world_size", meta.get("n_gpus", "?")))
+        # N = ranks (GPUs) when known: the reference's N was nodes with one rank each
+        n = meta.get("world_size", meta.get("n_gpus", meta.get("nnodes", "?")))
         label = f"N={n!s:>2}  dataset={meta.get('dataset', '?')!s:>6}  job={meta.get('job_id', os.path.basename(ld))}"
         right = f"train={t:.2f}s" if t == t else "train=NA"
         if wall is not None:

@@ -111,6 +111,13 @@ class _WgradBatch:
             except RuntimeError:
                 pass  # not inside backward: flushed by the next flush() call
 
+    def reset(self):
+        """Drop anything a failed backward left queued (e.g. an OOM after queue_callback): its
+        problems must not land in a later step's grads, and the flush callback must re-arm."""
+        self.arena = None
+        self.xs, self.ys, self.meta, self.ps, self.offs = [], [], [], [], []
+        self.cb = False
+
     def _final(self):
         self.cb = False
         if self.xs:
@@ -133,6 +140,11 @@ _WG = _WgradBatch()
 def flush_wgrads():
     """Launch the queued LoRA weight-gradient problems now (one grouped kernel)."""
     _WG.flush()
+
+
+def reset_wgrads():
+    """Start-of-step hygiene (trainer / graph capture): discard problems a raised backward queued."""
+    _WG.reset()
 
 
 class AdapterOps:

@@ -73,8 +73,12 @@ class DistContext:
     pp_ranks: List[int] = field(default_factory=list)
     timeout: Optional[object] = None        # collective timeout (watchdog) for every group
     dp_ranks: List[int] = field(default_factory=list)
-    pp_fwd_group: Optional[object] = None   # p2p: activations stage s -> s+1
-    pp_bwd_group: Optional[object] = None   # p2p: activation grads stage s+1 -> s
+    pp_fwd_group: Optional[object] = None   # p2p (MIFT_PP_P2P=shared): activations, whole replica
+    pp_bwd_group: Optional[object] = None   # p2p (MIFT_PP_P2P=shared): activation grads, whole replica
+    # p2p (default MIFT_PP_P2P=link): one 2-rank communicator per adjacent stage pair AND direction:
+    # link_*[0] is the link to the previous stage, link_*[1] to the next (None at the ends)
+    link_f: List[Optional[object]] = field(default_factory=lambda: [None, None])  # activations s -> s+1
+    link_b: List[Optional[object]] = field(default_factory=lambda: [None, None])  # grads s+1 -> s
 
     @property
     def is_main(self):
@@ -173,13 +177,23 @@ def build_grid(ctx: DistContext, pp: int):
         ranks = list(range(r * pp, (r + 1) * pp))
         multi = pp > 1 and world > 1
         g = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
-        # one p2p communicator per direction (activations s->s+1, gradients s+1->s): a receive
-        # posted early on one direction never queues behind the other direction's send
+        # replica-wide p2p communicators per direction (the round-2 layout, MIFT_PP_P2P=shared)
         gf = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
         gb = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
         if ctx.rank in ranks:
             ctx.pp_group, ctx.pp_ranks = g, ranks
             ctx.pp_fwd_group, ctx.pp_bwd_group = gf, gb
+        # per-link communicators (default): stage s's "recv from s-1" and "send to s+1" are on
+        # different communicators, hence different RCCL streams, so neither ever queues behind the
+        # other (pipeline.py, "p2p ordering")
+        for s in range(pp - 1) if multi else ():
+            pair = [ranks[s], ranks[s + 1]]
+            lf = dist.new_group(pair, timeout=ctx.timeout)
+            lb = dist.new_group(pair, timeout=ctx.timeout)
+            if ctx.rank == pair[0]:
+                ctx.link_f[1], ctx.link_b[1] = lf, lb
+            elif ctx.rank == pair[1]:
+                ctx.link_f[0], ctx.link_b[0] = lf, lb
     for s in range(pp):
         ranks = list(range(s, world, pp))
         g = dist.new_group(ranks, timeout=ctx.timeout) if dp > 1 and world > 1 else None
