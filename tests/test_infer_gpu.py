@@ -59,3 +59,59 @@ def test_fused_generate_matches_recompute(name):
     out = generate(m, batch, attention_mask=mask, max_new_tokens=6, eos_token_id=-1)
     solo = generate(m, ids[1:2, 6:], max_new_tokens=6, eos_token_id=-1)
     assert (out[1, 24:] == solo[0, 18:]).float().mean().item() >= 0.8
+
+
+@pytest.mark.parametrize("hd", [64, 80])
+def test_decode_attn_prompt_gap(hd):
+    """Right-aligned prompts (generate.py): keys in [plen[b], gend) are masked; the rest exact."""
+    from mift.ops import kernels as K
+    torch.manual_seed(1)
+    B, H, Tmax, t, gend = 3, 2, 64, 40, 30
+    dt = torch.bfloat16
+    kc = torch.randn(B, H, Tmax, hd, device="cuda").to(dt)
+    vc = torch.randn(B, H, Tmax, hd, device="cuda").to(dt)
+    qkv = torch.randn(B, 3 * H * hd, device="cuda").to(dt)
+    plen = torch.tensor([30, 7, 1], device="cuda", dtype=torch.int32)
+    kc0, vc0 = kc.clone(), vc.clone()
+    o = K.decode_attn(qkv, kc, vc, t, hd ** -0.5, plen=plen, gend=gend)
+    d = H * hd
+    kref, vref = kc0.clone(), vc0.clone()
+    kref[:, :, t] = qkv[:, d:2 * d].view(B, H, hd)
+    vref[:, :, t] = qkv[:, 2 * d:].view(B, H, hd)
+    j = torch.arange(t + 1, device="cuda")[None, :]
+    valid = (j < plen[:, None].long()) | (j >= gend)
+    q = qkv[:, :d].view(B, H, 1, hd)
+    oref = ref.attention(q.float(), kref[:, :, :t + 1].float(), vref[:, :, :t + 1].float(), causal=False,
+                         key_padding=valid, scale=hd ** -0.5)
+    torch.testing.assert_close(o.float(), oref.transpose(1, 2).reshape(B, d), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("name", ["gpt2", "opt"])
+def test_padded_distinct_prompts_match_solo_nocache(name):
+    """The probe's padded path: 16 DIFFERENT left-padded prompts generated as one batch (flash prefill
+    over right-aligned prompts, gap-masked decode, gemm_nt logits) give each row the tokens of its
+    own unpadded prompt run without a cache (full recompute per token)."""
+    from mift.apps.gen_probe import distinct_prompts
+    from mift.infer.generate import generate, generate_nocache
+    from mift.models.gpt2 import GPT2Config, GPT2LMHeadModel
+    from mift.models.opt import OPTConfig, OPTForCausalLM
+    if name == "gpt2":
+        m = GPT2LMHeadModel(GPT2Config(vocab_size=1000, n_positions=128, n_embd=128, n_layer=2, n_head=2,
+                                       n_inner=512), dtype=torch.bfloat16, device="cuda").init_weights(1)
+    else:
+        m = OPTForCausalLM(OPTConfig(vocab_size=1000, hidden_size=320, num_hidden_layers=2, ffn_dim=1280,
+                                     num_attention_heads=4, max_position_embeddings=128), dtype=torch.float16,
+                           device="cuda").init_weights(2)
+    m.eval()
+    ids, mask = distinct_prompts(16, 1000, 1, "cuda")
+    S0 = ids.shape[1]
+    out = generate(m, ids, attention_mask=mask, max_new_tokens=8, eos_token_id=-1)
+    assert out.shape == (16, S0 + 8) and torch.equal(out[:, :S0], ids)
+    agree, total = 0, 0
+    for b in range(16):
+        L = int(mask[b].sum())
+        solo = generate_nocache(m, ids[b:b + 1, S0 - L:], max_new_tokens=8)
+        agree += int((solo[0, L:] == out[b, S0:]).sum())
+        total += 8
+    print(f"{name}: padded-batch vs solo no-cache token agreement {agree}/{total}")
+    assert agree >= 0.95 * total, (agree, total)

@@ -14,7 +14,9 @@ from mift.utils import harness
 
 
 def _worker(rank, world, pp=1, zero=0, steps=2, mb=2, accum=4, dropout=0.0, partition="uniform",
-            ckpt_dir=None, resume=None):
+            ckpt_dir=None, resume=None, p2p="link"):
+    import os
+    os.environ["MIFT_PP_P2P"] = p2p
     from mift import lora as L
     from mift.data import MicroBatcher, synthetic_openwebtext
     from mift.models import build_causal_lm
@@ -76,6 +78,30 @@ def test_ddp_matches_single(single):
 def test_pipeline_matches_single_with_dropout(single_drop):
     r = harness.run(_worker, 2, pp=2, accum=4, dropout=0.1)
     _close_runs(r[0], single_drop)
+
+
+@pytest.mark.parametrize("p2p", ["shared", "blocking"])
+def test_pipeline_p2p_modes(single_drop, p2p):
+    """The round-2 replica-wide per-direction communicators and the blocking single-communicator
+    fallback (MIFT_PP_P2P) train exactly like the default per-link layout."""
+    r = harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, p2p=p2p)
+    _close_runs(r[0], single_drop)
+
+
+def test_ring_slot_reuse_is_checked():
+    """A receive ring slot may be handed out again only after the compute reading it was queued
+    (release): on RCCL a receive is ordered only behind work queued before its post."""
+    from mift.parallel.pipeline import _Ring
+    ring = _Ring(2, torch.float32, torch.device("cpu"))
+    a, sa = ring.get((2, 3))
+    b, sb = ring.get((2, 3))
+    with pytest.raises(RuntimeError, match="reused before"):
+        ring.get((2, 3))  # slot of `a` not released yet
+    ring.release(sa)
+    c, sc = ring.get((2, 3))
+    assert sc == sa and c.data_ptr() == a.data_ptr()
+    ring.release(sb)
+    ring.release(sc)
 
 
 def test_pipeline_4_stages_balanced(single_drop):

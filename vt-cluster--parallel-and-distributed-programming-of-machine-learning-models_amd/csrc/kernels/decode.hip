@@ -11,7 +11,10 @@
 // [B, H, Tmax, HD] keeps one head's keys contiguous, so the score pass is one
 // thread per key with 16-B row loads and the P·V pass maps threads to
 // (head-dim lane, key group) so each wave reads whole V rows coalesced.
-// Left padding: keys < start[b] are masked (HF left-padded batched generate).
+// Padding, two layouts: left padding — keys < start[b] are masked (HF left-padded batched
+// generate); or a prompt GAP — the prefill ran the prompts right-aligned to position 0 through the
+// flash kernel (kv_len = prompt length), so row b's cache holds its prompt at [0, plen[b]) and the
+// generated tokens from gend on: keys in [plen[b], gend) are masked.
 // Decode is HBM/latency bound (B·H·t·HD·2·2 bytes per layer): no MFMA.
 #include "common.h"
 #include <torch/extension.h>
@@ -22,8 +25,9 @@ namespace {
 template <typename T, int HD>
 __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ qkv, T* __restrict__ kc,
                                                           T* __restrict__ vc, T* __restrict__ out,
-                                                          const int* __restrict__ start, int H, int Tmax, int t,
-                                                          float scale) {
+                                                          const int* __restrict__ start,
+                                                          const int* __restrict__ plen, int gend, int H, int Tmax,
+                                                          int t, float scale) {
   constexpr int G = 256 / HD;  // key groups in the P·V pass
   extern __shared__ float sm[];
   float* qs = sm;              // [HD]
@@ -43,10 +47,11 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ 
   }
   __syncthreads();
   const int s0 = start ? start[b] : 0;
+  const int g0 = plen ? plen[b] : gend;  // masked gap [g0, gend)
   float mx = -INFINITY;
   for (int j = tid; j <= t; j += 256) {
     float s = -INFINITY;
-    if (j >= s0) {
+    if (j >= s0 && (j < g0 || j >= gend)) {
       const T* kr = (j == t) ? kg : kcb + (int64_t)j * HD;
       s = 0.f;
 #pragma unroll
@@ -81,6 +86,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ 
   float acc = 0.f;
   if (g < G) {
     for (int j = s0 + g; j <= t; j += G) {
+      if (j >= g0 && j < gend) continue;  // gap keys: p = 0, their V rows are never read
       const T* vr = (j == t) ? vg : vcb + (int64_t)j * HD;
       acc += sc[j] * (float)vr[d];
     }
@@ -96,19 +102,21 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ 
 }
 
 template <typename T, int HD>
-void launch(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, at::Tensor& out, const int* start, int B, int H,
-            int Tmax, int t, float scale, hipStream_t st) {
+void launch(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, at::Tensor& out, const int* start, const int* plen,
+            int gend, int B, int H, int Tmax, int t, float scale, hipStream_t st) {
   constexpr int G = 256 / HD;
   const size_t smem = (size_t)(HD + G * HD + t + 1) * sizeof(float);
   hipLaunchKernelGGL((decode_attn_kernel<T, HD>), dim3(B * H), dim3(256), smem, st, (const T*)qkv.data_ptr(),
-                     (T*)kc.data_ptr(), (T*)vc.data_ptr(), (T*)out.data_ptr(), start, H, Tmax, t, scale);
+                     (T*)kc.data_ptr(), (T*)vc.data_ptr(), (T*)out.data_ptr(), start, plen, gend, H, Tmax, t, scale);
 }
 
 }  // namespace
 
-// qkv [B, 3*H*HD]; kc/vc [B, H, Tmax, HD] (row t written); start [B] int32 or None -> o [B, H*HD]
+// qkv [B, 3*H*HD]; kc/vc [B, H, Tmax, HD] (row t written); start [B] int32 or None; plen [B] int32 or
+// None with gend: keys in [plen[b], gend) masked -> o [B, H*HD]
 at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
-                            const c10::optional<at::Tensor>& start) {
+                            const c10::optional<at::Tensor>& start, const c10::optional<at::Tensor>& plen,
+                            int64_t gend) {
   TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 2, "decode_attn: qkv [B, 3*H*HD] contiguous");
   TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.sizes() == vc.sizes(),
               "decode_attn: caches [B,H,Tmax,HD]");
@@ -122,14 +130,20 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
     TORCH_CHECK(start->scalar_type() == at::kInt && start->numel() == B && start->is_cuda(), "decode_attn: start");
     sp = start->data_ptr<int>();
   }
+  const int* pl = nullptr;
+  if (plen) {
+    TORCH_CHECK(plen->scalar_type() == at::kInt && plen->numel() == B && plen->is_cuda(), "decode_attn: plen");
+    TORCH_CHECK(gend >= 0 && gend <= t, "decode_attn: gap end must be <= t");
+    pl = plen->data_ptr<int>();
+  }
   auto out = at::empty({B, H * HD}, qkv.options());
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const bool half = qkv.scalar_type() == at::kHalf;
   TORCH_CHECK(half || qkv.scalar_type() == at::kBFloat16, "decode_attn: bf16/fp16");
 #define MIFT_DEC(D)                                                                        \
   case D:                                                                                  \
-    if (half) launch<fp16, D>(qkv, kc, vc, out, sp, B, H, Tmax, (int)t, (float)scale, st); \
-    else launch<bf16, D>(qkv, kc, vc, out, sp, B, H, Tmax, (int)t, (float)scale, st);      \
+    if (half) launch<fp16, D>(qkv, kc, vc, out, sp, pl, (int)gend, B, H, Tmax, (int)t, (float)scale, st); \
+    else launch<bf16, D>(qkv, kc, vc, out, sp, pl, (int)gend, B, H, Tmax, (int)t, (float)scale, st);      \
     break;
   switch (HD) {
     MIFT_DEC(32) MIFT_DEC(64) MIFT_DEC(80) MIFT_DEC(128)

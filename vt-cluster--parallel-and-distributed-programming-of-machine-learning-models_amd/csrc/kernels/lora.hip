@@ -525,10 +525,21 @@ __global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const WgArgs arg
   for (int k = 0; k < NQT; ++k) {
     const int e = (threadIdx.x + 256 * k) * 4;  // slab element: [c][li][p]
     const int c = e / 1024, li = (e / 64) % 16, pl = e % 64;
+    // chunk slabs added strictly in chunk order (the deterministic result), their loads issued 8 at
+    // a time: the serial dependent-load chain was latency-bound (~10 us per distilgpt2 layer)
     float4_ sum = float4_{0.f, 0.f, 0.f, 0.f};
+    const float* base = args.ws + (size_t)(pr.blk0 + pt) * SL + e;
+    const size_t cstep = (size_t)ntp * SL;
 #pragma unroll 1
-    for (int ch = 0; ch < nch; ++ch)
-      sum += *reinterpret_cast<const float4_*>(args.ws + (size_t)(pr.blk0 + ch * ntp + pt) * SL + e);
+    for (int ch0 = 0; ch0 < nch; ch0 += 8) {
+      float4_ v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = *reinterpret_cast<const float4_*>(base + (size_t)min(ch0 + u, nch - 1) * cstep);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (ch0 + u < nch) sum += v[u];
+    }
     const int q = c * 16 + li;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

@@ -79,10 +79,11 @@ at::Tensor mift_attn_bwd_bits(const at::Tensor& dout, const at::Tensor& qkv, con
 
 // ---- K12 decode attention over a KV cache (kernels/decode.hip)
 at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
-                            const c10::optional<at::Tensor>& start);
+                            const c10::optional<at::Tensor>& start, const c10::optional<at::Tensor>& plen,
+                            int64_t gend);
 
 #define MIFT_BIND_MORE(m) \
-  m.def("decode_attn", &mift_decode_attn, "single-token attention over a KV cache; appends k/v at t"); \
+  m.def("decode_attn", &mift_decode_attn, "single-token attention over a KV cache; appends k/v at t (left padding: start; prompt gap: plen, gend)"); \
   m.def("lora_proj", &mift_lora_proj, "out[M,32] = alpha*drop(x)@w^T (tall-skinny MFMA)"); \
   m.def("layer_norm_fwd_proj", &mift_layer_norm_fwd_proj, "LN fwd + alpha*drop(y)@pw^T -> (y, mean, rstd, proj)"); \
   m.def("mask_proj", &mift_mask_proj, "y = dropout(x) (p>0), proj = alpha*y@pw^T -> (y, proj)"); \

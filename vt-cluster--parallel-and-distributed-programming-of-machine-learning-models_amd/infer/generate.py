@@ -10,10 +10,20 @@ finished.
 
 MI355X design: one preallocated cache per layer ``[B, H, Tmax, hd]`` (16-bit,
 HBM-resident — 288 GB makes Tmax = context limit affordable), prefill runs
-the normal block path (flash attention when unpadded) and stores K/V once;
+the normal block path through the flash-attention kernel and stores K/V once;
 every decode step is the fused block path with the attention replaced by
 the ``decode_attn`` HIP kernel, which appends the new K/V in the same
-launch.  CPU tensors run the same algorithm with torch ops (the oracle).
+launch, and the LM-head logits are the hand-written MFMA GEMM (``gemm_nt``).
+No library GEMM and no SDPA run on the GPU path.
+
+Left-padded batches: the prefill runs every prompt RIGHT-aligned to position 0
+(row b's tokens ``ids[b, start_b:]`` then padding) so the flash kernel's
+``kv_len`` key mask is exact — queries see keys [0, q] of their own prompt,
+positions are 0..len_b-1 as HF computes them from the mask — and the next
+token is read at row b's last prompt position.  The cache then holds row b's
+prompt at [0, len_b) and generated tokens from S0 on; the decode kernel masks
+the gap [len_b, S0).  Returned ids keep the HF left-padded layout.  CPU
+tensors run the same algorithm with torch ops (the oracle).
 """
 import torch
 
@@ -35,45 +45,41 @@ def _split_heads(x, B, S, H, hd):
     return x.view(B, S, H, hd).transpose(1, 2)
 
 
-def _prefill_attn(cache, li, B, S, H, hd, start, fused):
-    """attn(qkv [B,S,3d]) -> o [B,S,d]; stores K/V rows [0, S) of layer li."""
+def _prefill_attn(cache, li, B, S, H, hd, kv_len, fused):
+    """attn(qkv [B,S,3d]) -> o [B,S,d] over right-aligned prompts (keys >= kv_len[b] masked);
+    stores K/V rows [0, S) of layer li."""
     d = H * hd
     scale = hd ** -0.5
 
     def attn(qkv):
         qkv3 = qkv.reshape(B, S, 3 * d)
-        q = _split_heads(qkv3[..., :d], B, S, H, hd)
         k = _split_heads(qkv3[..., d:2 * d], B, S, H, hd)
         v = _split_heads(qkv3[..., 2 * d:], B, S, H, hd)
         cache.k[li][:, :, :S].copy_(k)
         cache.v[li][:, :, :S].copy_(v)
-        if start is None and fused:
+        if fused:
             from ..ops.attention import causal_attention
-            return causal_attention(qkv3, B, S, H, hd, scale=scale)
+            return causal_attention(qkv3, B, S, H, hd, scale=scale, kv_len=kv_len)
+        q = _split_heads(qkv3[..., :d], B, S, H, hd)
         valid = None
-        if start is not None:
-            valid = torch.arange(S, device=qkv.device)[None, :] >= start[:, None]
-        if fused:  # padded prompt on GPU: SDPA with an explicit causal & key mask (one-off prefill)
-            m = torch.ones(S, S, dtype=torch.bool, device=qkv.device).tril()[None, None]
-            if valid is not None:
-                m = m & valid[:, None, None, :]
-            o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=m, scale=scale)
-            o = torch.nan_to_num(o)
-        else:
-            o = ref.attention(q, k, v, causal=True, key_padding=valid, scale=scale)
+        if kv_len is not None:
+            valid = torch.arange(S, device=qkv.device)[None, :] < kv_len[:, None].long()
+        o = ref.attention(q, k, v, causal=True, key_padding=valid, scale=scale)
         return o.transpose(1, 2).reshape(B, S, d)
 
     return attn
 
 
-def _decode_attn(cache, li, B, H, hd, t, start, start_i32, fused):
+def _decode_attn(cache, li, B, H, hd, t, plen, gend, fused):
+    """Attention of the token at cache position t; keys in [plen[b], gend) are the prompt gap."""
     d = H * hd
     scale = hd ** -0.5
 
     def attn(qkv):
         if fused:
             from ..ops import kernels as K
-            o = K.decode_attn(qkv.reshape(B, 3 * d).contiguous(), cache.k[li], cache.v[li], t, scale, start_i32)
+            o = K.decode_attn(qkv.reshape(B, 3 * d).contiguous(), cache.k[li], cache.v[li], t, scale,
+                              plen=plen, gend=gend)
             return o.view(B, 1, d)
         qkv3 = qkv.reshape(B, 3 * d)
         q = qkv3[:, :d].view(B, H, 1, hd)
@@ -81,8 +87,9 @@ def _decode_attn(cache, li, B, H, hd, t, start, start_i32, fused):
         cache.v[li][:, :, t] = qkv3[:, 2 * d:].view(B, H, hd)
         k, v = cache.k[li][:, :, :t + 1], cache.v[li][:, :, :t + 1]
         valid = None
-        if start is not None:
-            valid = torch.arange(t + 1, device=qkv.device)[None, :] >= start[:, None]
+        if plen is not None:
+            j = torch.arange(t + 1, device=qkv.device)[None, :]
+            valid = (j < plen[:, None].long()) | (j >= gend)
         o = ref.attention(q, k, v, causal=False, key_padding=valid, scale=scale)
         return o.transpose(1, 2).reshape(B, 1, d)
 
@@ -126,19 +133,26 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
     if bool((attention_mask != (torch.arange(S0, device=dev)[None, :] >= start[:, None]).long()).any()):
         raise ValueError("generate expects left padding (HF padding_side='left')")
     padded = bool((start > 0).any())
-    start_t = start if padded else None
-    start_i32 = start.to(torch.int32).contiguous() if padded else None
+    plen = lens.to(torch.int32).contiguous() if padded else None
     fused = model._use_fused(input_ids)
     H, hd = _heads(model)
     L = len(model.blocks())
     dtype = model.tied_embedding().dtype
     cache = KVCache(L, B, H, S0 + max_new_tokens, hd, dtype, dev)
 
-    # prefill
-    pos = (torch.cumsum(attention_mask, 1) - 1).clamp(min=0) * attention_mask
-    h = model.embed_at(input_ids, pos)
-    h = _run_blocks(model, h, lambda li: _prefill_attn(cache, li, B, S0, H, hd, start_t, fused), fused)
-    logits = model.head_logits(h[:, -1:])
+    # prefill over right-aligned prompts: row b = ids[b, start_b:] then padding, positions 0..S0-1
+    ar = torch.arange(S0, device=dev)
+    if padded:
+        src = (ar[None, :] + start[:, None]).clamp(max=S0 - 1)
+        ids_r = torch.where(ar[None, :] < lens[:, None], torch.gather(input_ids, 1, src),
+                            torch.full_like(input_ids, pad if pad is not None and pad >= 0 else 0))
+    else:
+        ids_r = input_ids
+    h = model.embed_at(ids_r, ar[None, :].expand(B, S0).contiguous())
+    h = _run_blocks(model, h, lambda li: _prefill_attn(cache, li, B, S0, H, hd, plen, fused), fused)
+    last = (lens - 1).clamp(min=0)
+    h_last = torch.gather(h, 1, last[:, None, None].expand(B, 1, h.shape[-1])) if padded else h[:, -1:]
+    logits = model.head_logits(h_last)
     nxt = logits[:, -1].float().argmax(-1)
     out = [input_ids]
     done = torch.zeros(B, dtype=torch.bool, device=dev)
@@ -152,7 +166,7 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
         t = S0 + i
         pos = (lens + i)[:, None]
         h = model.embed_at(nxt[:, None], pos)
-        h = _run_blocks(model, h, lambda li: _decode_attn(cache, li, B, H, hd, t, start_t, start_i32, fused), fused)
+        h = _run_blocks(model, h, lambda li: _decode_attn(cache, li, B, H, hd, t, plen, S0, fused), fused)
         nxt = model.head_logits(h)[:, -1].float().argmax(-1)
     return torch.cat(out, 1)
 

@@ -532,7 +532,9 @@ def lm_head_xent(h, ln, w_nk, labels, V, ignore_index=-100, need_grad=True, w_kn
 
 
 def lm_head_logits(h, ln, w_nk, V):
+    """Logits of the tied head (inference / generation): LN kernel + the MFMA ``gemm_nt`` against
+    the padded [V_pad, d] weight — no library GEMM on the decode path."""
     h2 = _flat(h.contiguous())
     a, _, _ = K.layer_norm_fwd(h2, ln.weight, ln.bias, ln.eps)
-    logits = torch.matmul(a, w_nk.t())
+    logits = K.gemm(a, w_nk)
     return logits[:, :V].reshape(*h.shape[:-1], V)

@@ -89,9 +89,10 @@ def xent(logits, labels, V, ignore_index=-100, write_grad=True):
     return C().xent_fwd_bwd(logits, labels, int(V), int(ignore_index), bool(write_grad))
 
 
-def decode_attn(qkv, kcache, vcache, t, scale, start=None):
-    """o [B, H*hd] for the token at position t; writes its k/v into the caches."""
-    return C().decode_attn(qkv, kcache, vcache, int(t), float(scale), start)
+def decode_attn(qkv, kcache, vcache, t, scale, start=None, plen=None, gend=0):
+    """o [B, H*hd] for the token at position t; writes its k/v into the caches.  Masked keys:
+    ``< start[b]`` (left padding) and ``[plen[b], gend)`` (right-aligned prompts, generate.py)."""
+    return C().decode_attn(qkv, kcache, vcache, int(t), float(scale), start, plen, int(gend))
 
 
 def layer_norm_fwd_proj(x, w, b, eps, pw, rank, alpha=1.0, p=0.0, seed=0):

@@ -28,8 +28,10 @@ design that also fixes its defects:
     FIFO and an early-posted receive can only wait for ITS send: stage s's "send y(i) to s+1"
     never queues behind its "recv x(i+1) from s-1" (round 2 put both on one replica-wide
     communicator per direction, coupling y(i) to the predecessor's next forward — VERDICT r2
-    weak #6; kept as ``MIFT_PP_P2P=shared``).  ``MIFT_PP_P2P=blocking`` completes every exchange
-    on the replica communicator before compute continues (no prefetch; the debugging fallback).
+    weak #6; kept as ``MIFT_PP_P2P=shared``).  ``MIFT_PP_P2P=blocking`` is the debugging fallback:
+    one replica communicator, every receive posted just in time and completed before its
+    consumer (no prefetch); sends stay asynchronous (blocking sends deadlock 1F1B: s blocked
+    sending y(i) to s+1 while s+1 is blocked sending dX(j) to s).
     Deadlock freedom: receives are asynchronous and the compute stream waits on one only right
     before its consumer; the matching send precedes that consumer in the 1F1B dependency graph,
     which is acyclic.  RCCL makes a p2p's stream wait for the compute stream at POST time, so a
@@ -169,7 +171,7 @@ class PipelineEngine:
 
     def _post(self, p2p, **kw):
         pend = p2p.post(**kw)
-        if self.blocking:
+        if self.blocking and kw.get("recvs"):
             pend.wait()
         return pend
 
@@ -199,6 +201,7 @@ class PipelineEngine:
         live = deque()
         xq = deque()
         sends = []
+        pre = not self.blocking  # prefetch receives ahead of the compute that needs them
 
         def post_x(i):
             if not self.first and i < M:
@@ -208,6 +211,8 @@ class PipelineEngine:
         def take_x(i):
             if self.first:
                 return None, None
+            if not pre:
+                post_x(i)
             pend, slot = xq.popleft()
             pend.wait()
             return run.x_input(i, slot), slot
@@ -225,6 +230,8 @@ class PipelineEngine:
             return y
 
         def bwd(b, gp):
+            if gp is None and not pre:
+                gp = post_g(b)
             bx, by, xslot = live.popleft()
             g = None
             if gp is not None:
@@ -238,21 +245,24 @@ class PipelineEngine:
                 sends.append(run.send_gx(b, self._post(self.tx_b, sends=[(gx, self.prev)])))
             run.release_x(b, bx, xslot)
 
-        post_x(0)
+        if pre:
+            post_x(0)
         for i in range(nwarm):
             x, xs = take_x(i)
-            post_x(i + 1)
+            if pre:
+                post_x(i + 1)
             live.append((x, fwd(i, x), xs))
         for j in range(nsteady):
             i = nwarm + j
-            gp = post_g(j)          # grad of the oldest live micro-batch, requested before the forward
+            gp = post_g(j) if pre else None  # grad of the oldest live micro-batch, requested before the forward
             x, xs = take_x(i)
-            post_x(i + 1)
+            if pre:
+                post_x(i + 1)
             live.append((x, fwd(i, x), xs))
             bwd(j, gp)
         for k in range(nwarm):
             b = nsteady + k
-            bwd(b, post_g(b))
+            bwd(b, post_g(b) if pre else None)
         for p in sends:
             if p is not None:
                 p.wait()
@@ -322,13 +332,13 @@ class _Ring:
         shape = tuple(shape)
         bufs = self.bufs.setdefault(shape, [])
         i = self.idx.get(shape, 0)
-        self.idx[shape] = i + 1
-        if len(bufs) < self.n:
-            bufs.append(torch.empty(shape, dtype=self.dtype, device=self.device))
         slot = (shape, i % self.n)
         if self.busy.get(slot):
             raise RuntimeError(f"pipeline {self.what} ring slot {slot[1]} reused before the compute reading it "
                                f"was queued (ring of {self.n})")
+        self.idx[shape] = i + 1
+        if len(bufs) < self.n:
+            bufs.append(torch.empty(shape, dtype=self.dtype, device=self.device))
         self.busy[slot] = True
         # a fresh leaf view per use: no autograd state (.grad, requires_grad) carries over
         return bufs[slot[1]].detach(), slot
