@@ -185,6 +185,7 @@ def test_flash_attention_whole_sequence_kernels(S, p, dt, monkeypatch):
     """The whole-sequence-in-LDS kernels (MIFT_ATTN_SEQ=2 forces them at this small head count)
     against the fp32 reference, and bit-for-bit agreement of fwd with the tiled kernel."""
     monkeypatch.setenv("MIFT_ATTN_SEQ", "2")
+    monkeypatch.setenv("MIFT_ATTN_FWD", "1")  # bitwise seq-vs-tiled check of the v1 pair (v2: below)
     test_flash_attention_fwd_bwd(64, S, p, dt)
     C = _C()
     B, H, hd = 2, 3, 64
@@ -224,6 +225,36 @@ def test_attention_keep_bits_match_hash(hd, S, dt, monkeypatch):
         torch.testing.assert_close(d_bits, d_hash, atol=0, rtol=0)
         if hd == 64:
             assert bits.numel() == B * H * S * ((S + 63) // 64 * 4)  # the record exists on this path
+
+
+@pytest.mark.parametrize("hd", [64, 80, 128])
+@pytest.mark.parametrize("S", [512, 200])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_fwd_v2(hd, S, p, monkeypatch):
+    """v2 forward (32x32x16 MFMA, 32 queries per wave, hd 80 QK^T without padding) against the fp32
+    reference incl. right padding, and its keep-bit record (written on the whole-sequence geometry)
+    read by the backward == the re-hashing backward, bit for bit."""
+    monkeypatch.setenv("MIFT_ATTN_FWD", "2")
+    C = _C()
+    torch.manual_seed(3 + hd)
+    B, H = 2, 3
+    dt = torch.float16 if hd == 80 else torch.bfloat16
+    qkv = torch.randn(B * S, 3 * H * hd, device="cuda").to(dt)
+    kvl = torch.tensor([S - 21, S // 3], device="cuda", dtype=torch.int32)
+    for lens in (None, kvl):
+        o, lse = C.attn_fwd(qkv, B, S, H, hd, hd ** -0.5, p, 55, lens)
+        oref = _attn_ref(qkv, B, S, H, hd, hd ** -0.5, p, 55, lens)
+        torch.testing.assert_close(o.float(), oref, atol=3e-2, rtol=3e-2)
+        assert torch.isfinite(lse).all() or lens is not None
+    if p > 0 and S <= 256 or hd == 64:
+        monkeypatch.setenv("MIFT_ATTN_SEQ", "2")
+        for lens in (None, kvl):
+            o, lse, bits = C.attn_fwd_bits(qkv, B, S, H, hd, hd ** -0.5, p, 77, lens)
+            do = torch.randn_like(o)
+            d_hash = C.attn_bwd(do, qkv, o, lse, B, S, H, hd, hd ** -0.5, p, 77, lens)
+            d_bits = C.attn_bwd_bits(do, qkv, o, lse, B, S, H, hd, hd ** -0.5, p, 77, lens,
+                                     bits if bits.numel() else None)
+            torch.testing.assert_close(d_bits, d_hash, atol=0, rtol=0)
 
 
 def test_flash_attention_kv_len():

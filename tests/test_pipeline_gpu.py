@@ -50,6 +50,9 @@ def _close(a, b, tol):
     assert len(a["loss"]) == len(b["loss"]) == 3
     for x, y in zip(a["loss"], b["loss"]):
         assert abs(x - y) <= tol * max(1.0, abs(y)), (a["loss"], b["loss"])
+    # grad norms every step: a replay that produced inf/NaN grads shows as a skipped step (norm 0)
+    for x, y in zip(a["gn"], b["gn"]):
+        assert y > 0 and abs(x - y) <= 2e-2 * y, (a["gn"], b["gn"])
     assert a["state"].keys() == b["state"].keys() and a["state"]
     for k in a["state"]:
         d = (a["state"][k] - b["state"][k]).abs().max().item()

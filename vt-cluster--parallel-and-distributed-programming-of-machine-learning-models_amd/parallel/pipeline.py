@@ -357,14 +357,17 @@ class _StageGraphs:
     micro-batch inputs, the received activation x_k (a leaf that requires grad), the micro-step
     counter read by every dropout kernel (csrc/common.h ``mift_seed``), the forward output y_k
     (held with its autograd graph: the saved activations stay allocated), the received gradient
-    g_k and the backward output dX_k = x_k.grad.  All slots share one private memory pool."""
+    g_k and the backward output dX_k = x_k.grad.  Every slot has its OWN private memory pool: graphs
+    that share a pool must replay in capture order (a block freed at the end of one capture is handed
+    to the next), but 1F1B replays F(i+1) before B(i) — with one shared pool the backward of slot k
+    overwrote slot k+1's saved activations (measured: NaN gradients from the first replayed step).
+    Within a slot the order is the capture order (forward, then backward)."""
 
     def __init__(self, eng):
         self.e = eng
         self.sig = None
         self.seen = set()
         self.slots = None
-        self.pool = None
         self.gs = torch.zeros((), dtype=torch.float32, device=eng.device)
 
     @staticmethod
@@ -413,11 +416,9 @@ class _StageGraphs:
                             m._mpack = None
                 C().set_seed_step(sl["step"])
                 gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gf, pool=self.pool, capture_error_mode="thread_local"):
+                with torch.cuda.graph(gf, capture_error_mode="thread_local"):
                     y = e._forward(sl["inp"], sl.get("x"), 0)
-                if self.pool is None:
-                    self.pool = gf.pool()
-                with torch.cuda.graph(gb, pool=self.pool, capture_error_mode="thread_local"):
+                with torch.cuda.graph(gb, pool=gf.pool(), capture_error_mode="thread_local"):
                     if e.last:
                         (y * self.gs).backward(retain_graph=True)
                     else:
@@ -430,8 +431,7 @@ class _StageGraphs:
             graph_seeds(False)
             streams.set_enabled(None)
             C().set_seed_step(None)
-        e.stats["fwd"] -= K
-        e.stats["bwd"] -= K
+        e.stats["fwd"] -= K  # the captures ran _forward once per slot (backward bypassed _backward)
         torch.cuda.synchronize(e.device)
 
 
