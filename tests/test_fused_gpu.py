@@ -127,6 +127,28 @@ def test_opt_fused_matches_reference(dtype, p):
     _grad_close(ref, fused, 5e-2 if dtype == torch.float16 else 1.2e-1)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_opt_fused_grads_within_5pct_away_from_relu_kinks(dtype):
+    """The bf16 tolerance above (12 %) is ReLU-derivative flips: fc1 pre-activations within 16-bit
+    rounding of 0 take opposite branches in the fp32 reference and the bf16 kernels.  Push every
+    pre-activation away from the kink (fc1 bias = ±4, so |z| >> rounding) and the same comparison
+    holds within 5 % for bf16 too — the fused backward itself is as exact as fp16 (VERDICT r2 #8)."""
+    cfg, ref, fused = _opt_models(dtype, 0.0, lora_p=0.0)
+    with torch.no_grad():
+        for m_ in (ref, fused):
+            for n, q in m_.named_parameters():
+                if n.endswith("fc1.bias"):
+                    sgn = torch.where(torch.arange(q.numel(), device=q.device) % 2 == 0, 4.0, -4.0)
+                    q.copy_(sgn.to(q.dtype))
+    torch.manual_seed(1)
+    ids = torch.randint(3, cfg.vocab_size, (3, 96), device="cuda")
+    ref.train()
+    fused.train()
+    ref(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
+    fused(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
+    _grad_close(ref, fused, 5e-2)
+
+
 def test_opt_arena_multi_adapter_matches_dense():
     from mift.lora import LoraArena
     from mift.lora.pack import attach

@@ -30,3 +30,23 @@ def test_layout_disjoint_aligned_roundtrip():
         assert torch.equal(buf[off:off + n].view(dt).view(shp), mbs[i][k])
     assert buf[steps_off:steps_off + 24].view(torch.int64).tolist() == [11, 12, 13]
     assert buf[inv_off:inv_off + 4].view(torch.float32).item() == 0.125
+
+
+def test_capture_invalidates_multi_adapter_pack():
+    """OPT's q/k/v adapters share one K-extension cached on a ConcatLinear (not an nn.Module). A
+    hipGraph capture taken right after an eager pass at the same arena version must rebuild that
+    operand inside the graph, otherwise every replay reads the pre-update LoRA weights (round-3
+    bug: graphed OPT drifted from eager from step 2).  CPU: only the cache bookkeeping is checked."""
+    from mift import lora as L
+    from mift.models import build_causal_lm
+    from mift.ops.fused import MultiAdapterOps, invalidate_packs
+    m = build_causal_lm("opt-tiny", dtype=torch.float32, seed=0)
+    L.inject(m, L.LoraConfig(r=8, lora_alpha=16, target_modules=["q_proj", "k_proj", "v_proj"]))
+    L.LoraArena(m)
+    cat = m.model.decoder.layers[0].self_attn.qkv
+    a = MultiAdapterOps(cat, torch.float32)
+    b = MultiAdapterOps(cat, torch.float32)
+    assert b.A32s is a.A32s  # same arena version, no capture in between: cached
+    invalidate_packs(m)
+    c = MultiAdapterOps(cat, torch.float32)
+    assert c.A32s is not a.A32s and torch.equal(c.A32s, a.A32s)

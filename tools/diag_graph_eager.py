@@ -53,7 +53,15 @@ def run(model_name, precision, steps, graph, warm):
         gns.append(st["grad_norm"])
         infs.append(st["found_inf"])
         params.append(tr.arena.param.detach().clone())
-    return {"loss": losses, "gn": gns, "inf": infs, "grads": grads, "params": params}
+    names = [(n, o, p.numel()) for (n, p), o in zip(tr.arena.named, tr.arena.offsets)]
+    return {"loss": losses, "gn": gns, "inf": infs, "grads": grads, "params": params, "names": names}
+
+
+def worst(a, b, names, k=4):
+    """The k parameters whose slices differ most between two flat arena tensors."""
+    d = (a - b).abs()
+    per = sorted(((float(d[o:o + n].max()), nm) for nm, o, n in names), reverse=True)[:k]
+    return [(nm, round(v, 6)) for v, nm in per if v > 0]
 
 
 def main():
@@ -66,11 +74,15 @@ def main():
             "eager2": run(a.model, a.precision, a.steps, False, True),
             "graph": run(a.model, a.precision, a.steps, True, True),
             "graph_nowarm": run(a.model, a.precision, a.steps, True, False)}
+    if a.precision == "fp16":
+        os.environ["MIFT_DIAG_NOREBIND"] = "1"
+        runs["graph_norebind"] = run(a.model, a.precision, a.steps, True, True)
     base = runs["eager"]
     for name, r in runs.items():
         rec = {"run": name, "loss": r["loss"], "gn": r["gn"], "found_inf": r["inf"]}
         rec["max_dgrad"] = [float((g - g0).abs().max()) for g, g0 in zip(r["grads"], base["grads"])]
         rec["max_dparam"] = [float((p - p0).abs().max()) for p, p0 in zip(r["params"], base["params"])]
+        rec["worst_grad"] = [worst(g, g0, r["names"]) for g, g0 in zip(r["grads"], base["grads"])]
         print(json.dumps(rec), flush=True)
 
 

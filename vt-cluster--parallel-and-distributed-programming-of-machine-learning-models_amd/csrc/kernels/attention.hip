@@ -988,9 +988,15 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
   char* Qs = smem;                          // Q rows (A of S; tr-read B of dK); lse·log2e in the row padding
   char* dOs = smem + (size_t)SP * G::RS;    // dO rows (A of dP; tr-read B of dV); D in the row padding
   constexpr int PADOFF = G::HDP * 2;        // first padding byte of a row (RS - HDP*2 >= 32)
-  static_assert(G::RS - PADOFF >= 4, "row padding holds one float");
-  auto lse_at = [&](int q) { return *reinterpret_cast<const float*>(Qs + (size_t)q * G::RS + PADOFF); };
-  auto D_at = [&](int q) { return *reinterpret_cast<const float*>(dOs + (size_t)q * G::RS + PADOFF); };
+  static_assert(G::RS - PADOFF >= 32, "32-B row padding");
+  // Byte x of row q's 32-B padding sits at (x + 16·((q >> 2) & 1)) mod 32: the two half-wave lane
+  // groups of a padding read address rows q and q + 4 (g = 0, 1), whose rows are a multiple of
+  // 128 B apart, so unrotated they hit the same bank with different addresses (2-way on every lse /
+  // D / keep-bit read: 3.1 M conflict cycles per distilgpt2 dispatch); rotated by 16 B
+  // the two groups use disjoint banks.
+  auto pad = [&](char* img, int q, int x) { return img + (size_t)q * G::RS + PADOFF + ((x + 16 * ((q >> 2) & 1)) & 31); };
+  auto lse_at = [&](int q) { return *reinterpret_cast<const float*>(pad(Qs, q, 0)); };
+  auto D_at = [&](int q) { return *reinterpret_cast<const float*>(pad(dOs, q, 0)); };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, kc = lane & 15;
@@ -1010,16 +1016,14 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
   stage_rows<T, HD>(dOs, dOg, D, S, SP, tid, NT);
   for (int i = tid; i < SP; i += NT) {
     const int q = min(i, S - 1);
-    *reinterpret_cast<float*>(Qs + (size_t)i * G::RS + PADOFF) = lse[(int64_t)bh * S + q] * LOG2E;
-    *reinterpret_cast<float*>(dOs + (size_t)i * G::RS + PADOFF) = Dv[(int64_t)bh * S + q];
+    *reinterpret_cast<float*>(pad(Qs, i, 0)) = lse[(int64_t)bh * S + q] * LOG2E;
+    *reinterpret_cast<float*>(pad(dOs, i, 0)) = Dv[(int64_t)bh * S + q];
   }
   // keep-bit records of the forward (KEEP BITS), element e of query q after the lse (e < 14) or the
   // D (e >= 14) float of row q: 28 B of padding per image row
   const int NR = SP / 16;
   const bool mk = dmask != nullptr;
-  auto rec_at = [&](int q, int e) -> char* {
-    return (e < 14 ? Qs + (size_t)q * G::RS + PADOFF + 4 + e * 2 : dOs + (size_t)q * G::RS + PADOFF + 4 + (e - 14) * 2);
-  };
+  auto rec_at = [&](int q, int e) -> char* { return e < 14 ? pad(Qs, q, 4 + e * 2) : pad(dOs, q, 4 + (e - 14) * 2); };
   if (mk) {
     MIFT_ASSERT(NR <= 28);
     for (int i = tid; i < S * (NR / 4); i += NT) {

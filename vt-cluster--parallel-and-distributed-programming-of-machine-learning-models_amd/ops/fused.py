@@ -194,6 +194,23 @@ class AdapterOps:
         return [dAf[:, :r].t(), dBf[:, :r]], dT32
 
 
+# Generation of the cached multi-adapter operands: bumped before every hipGraph capture so the
+# capture rebuilds them inside the graph (the cache key also holds the arena version, but a capture
+# taken right after an eager pass at the SAME version would otherwise bake the eager pass's
+# operands in, and every replay would read those stale pre-update values).  ConcatLinear is not an
+# nn.Module, so a walk over model.modules() cannot find and clear its cache (the round-3 bug:
+# graphed OPT runs drifted from eager from step 2 on).
+_PACK_GEN = [0]
+
+
+def invalidate_packs(model=None):
+    """Force every per-step LoRA operand pack to be rebuilt by its next use (call before a capture)."""
+    _PACK_GEN[0] += 1
+    pk = getattr(model, "_lora_pack", None) if model is not None else None
+    if pk is not None:
+        pk.version = -1
+
+
 class MultiAdapterOps:
     """Several adapters on projections that share one input (OPT q/k/v), as
     ONE K-extension: the 32 LoRA columns are split into equal slots, adapter j
@@ -219,7 +236,7 @@ class MultiAdapterOps:
         first = members[0][0]
         self.p = first.lora_dropout
         self.arena = getattr(first, "_arena", None)
-        key = (self.arena.version if self.arena is not None else None, dtype)
+        key = (self.arena.version if self.arena is not None else None, dtype, _PACK_GEN[0])
         cached = getattr(cat, "_mpack", None)
         if self.arena is not None and cached is not None and cached[0] == key:
             self.A32s, self.B32, self.B32t, self.At32 = cached[1]

@@ -390,10 +390,10 @@ class _StageGraphs:
         from ..models.layers import graph_seeds
         from ..ops import streams
         from ..ops.dispatch import C
+        from ..ops.fused import invalidate_packs
         e = self.e
         K = e.K
         self.slots = []
-        pk = getattr(e.model, "_lora_pack", None)
         torch.cuda.synchronize(e.device)
         graph_seeds(True)
         streams.set_enabled(False)
@@ -409,11 +409,7 @@ class _StageGraphs:
                 if not e.last:
                     sl["g"] = torch.zeros(e._act_shape(mbs[0]), dtype=e.dtype, device=e.device)
                 if k == 0:  # the per-step LoRA operand pack is captured into slot 0's forward
-                    if pk is not None:
-                        pk.version = -1
-                    for m in e.model.modules():
-                        if hasattr(m, "_mpack"):
-                            m._mpack = None
+                    invalidate_packs(e.model)
                 C().set_seed_step(sl["step"])
                 gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gf, capture_error_mode="thread_local"):

@@ -122,12 +122,8 @@ class GraphedStep:
             for k, v in mb.items():
                 static[i][k].copy_(v)
         # force the per-step LoRA operand packing into the captured region
-        pk = getattr(model, "_lora_pack", None)
-        if pk is not None:
-            pk.version = -1
-        for m in model.modules():
-            if hasattr(m, "_mpack"):
-                m._mpack = None
+        from ..ops.fused import invalidate_packs
+        invalidate_packs(model)
         g = torch.cuda.CUDAGraph()
         ms0 = model.micro_step
         torch.cuda.synchronize()

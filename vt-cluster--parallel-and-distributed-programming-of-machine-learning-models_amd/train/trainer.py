@@ -165,7 +165,8 @@ class Trainer:
         model.micro_step = ms0
         g.seen.add(sig)
         g.prepare(mbs)
-        self.arena.rebind_grads()
+        if os.environ.get("MIFT_DIAG_NOREBIND") != "1":
+            self.arena.rebind_grads()
         self.arena.grad.zero_()
         if red is not None:
             red.begin_step()
