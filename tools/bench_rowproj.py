@@ -30,6 +30,7 @@ SHAPES = [  # (name, M, D, rank rows, dtype)
     ("opt.qkv.dT", 24576, 7680, 24, torch.float16),
     ("dgpt.c_attn.ln_proj", 8192, 768, 8, torch.bfloat16),
     ("dgpt.c_fc.dT", 8192, 3072, 8, torch.bfloat16),
+    ("opt125.qkv.ln_proj", 16384, 768, 28, torch.float16),
 ]
 
 
@@ -57,6 +58,13 @@ def main():
             row["mask_proj_us"] = round(t * 1e3, 1)
             t = timeit(lambda: K.mask_scale(x, 0.1, 7))
             row["mask_scale_us"] = round(t * 1e3, 1)
+            if D in (768, 1024):  # the MFMA 16-row form runs by default there; the row kernels for A/B
+                os.environ["MIFT_ROWPROJ_V"] = "1"
+                t = timeit(lambda: K.layer_norm_fwd_proj(x, lw, lb, 1e-5, w32, r, 1.0, 0.05, 7))
+                row["ln_fwd_proj_rowkernel_us"] = round(t * 1e3, 1)
+                t = timeit(lambda: K.mask_proj(x, 0.1, 7, w32, r, 1.0))
+                row["mask_proj_rowkernel_us"] = round(t * 1e3, 1)
+                os.environ.pop("MIFT_ROWPROJ_V")
         t = timeit(lambda: K.lora_proj(x, w32, 1.0, 0.05, 7))
         row["lora_proj_p_us"] = round(t * 1e3, 1)
         t = timeit(lambda: K.lora_proj(x, w32, 1.0, 0.0, 0))

@@ -5,7 +5,8 @@ Every rank of the pipeline (and DP) grid is its own process on the same GPU; the
 gloo (host-staged) instead of RCCL, but the engine, its 1F1B schedule, the per-link p2p layout,
 the ring buffers, the per-slot stage hipGraphs, the cross-stage grad-norm all-reduce and the
 DP all-reduce run exactly the production code path.  The same data / seeds are first trained
-by a single-process dp1 run; the PP run's loss and grad-norm trajectories must match it.
+by the same DP degree without pipelining (dp1 for PP4 / PP8, dp2 for 2dp×4pp); the PP run's loss
+and grad-norm trajectories must match it.
 
   python tools/rehearse_pp.py --model facebook/opt-2.7b --pp 4 [--dp 1] --seq 512 --mb 4 --accum 24 --steps 3
 
@@ -90,9 +91,12 @@ def main():
            "transport": "gloo (one GPU, every rank its own process)"}
     t = time.perf_counter()
     if not a.skip_ref:
-        ref = harness.run(_worker, 1, env=env, timeout=a.timeout, pp=1, **kw)[0]
-        out["dp1"] = ref
-        print(f"dp1 done in {time.perf_counter() - t:.1f}s: {ref['loss']}", file=sys.stderr, flush=True)
+        # reference: the same DP degree without pipelining (dp1 for a pure PP grid).  A dp2 grid
+        # shards the data by replica, so its steps see other lines than a dp1 run's steps would.
+        ref = harness.run(_worker, a.dp, env=env, timeout=a.timeout, pp=1, **kw)[0]
+        out[f"dp{a.dp}"] = ref
+        print(f"dp{a.dp} reference done in {time.perf_counter() - t:.1f}s: {ref['loss']}", file=sys.stderr,
+              flush=True)
     t = time.perf_counter()
     res = harness.run(_worker, a.pp * a.dp, env=env, timeout=a.timeout, pp=a.pp, **kw)
     last = res[a.pp - 1]  # the last stage of replica 0 holds the loss; every rank logs the global one

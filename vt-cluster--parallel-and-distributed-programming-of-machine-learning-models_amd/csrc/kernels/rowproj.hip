@@ -220,6 +220,174 @@ __global__ __launch_bounds__(256) void mask_proj_kernel(const T* __restrict__ x,
   reduce_store<T, LR>(acc, pout + (size_t)row * 32, lane, alpha);
 }
 
+// ---- MFMA form (D = 32·NK, NK in {24, 32}): one 4-wave block per 16 rows ----
+// The one-wave-per-row kernels above re-read the [LR, D] projection operand from cache for every
+// row and do LR dot2 per element pair on the VALU: at LR = 32 (OPT's three q/k/v adapters) they
+// ran 136 us at M = 16384, D = 768, 10x the LN alone.  Here a block owns a 16-row MFMA A-tile and
+// its 4 waves split the k-steps (NK/4 each, 32 columns per k-step): lane (fr = lane & 15,
+// g = lane >> 4) of wave w holds row fr's columns 32·s + 8·g .. +7 of the wave's k-steps s, so
+//   * row statistics = per-lane partials + 2 cross-lane steps (xor 16, 32) + one LDS exchange of
+//     the 4 waves' [16] partials (two for LN: mean, then the centred sum of squares);
+//   * the row is normalised / masked in registers and stored as 16-B pieces;
+//   * the projection is NK/4 (rank <= 16) or 2·NK/4 MFMA 16x16x32 per wave on weight fragments
+//     read straight from global (L2 hits), reduced over the waves through LDS.
+// A first version with one wave per 16 rows (whole row per wave) had 2 waves per CU at
+// M = 8192 and ran 18.5 us against 7.1 us for the plain LN (latency-bound: one long chain per
+// wave).  Same numerics as the row kernels: y rounded to T before it is projected, dropped
+// elements zeroed (1/(1-p) folded into alpha by the host for LN), fp32 accumulation.
+template <typename T, typename W, int NK, int NTI, bool LN>
+__global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__ x, const W* __restrict__ lw,
+                                                           const W* __restrict__ lb, T* __restrict__ y,
+                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                           const T* __restrict__ pw, T* __restrict__ pout, int M,
+                                                           float eps, float alpha, uint64_t seed,
+                                                           const int64_t* __restrict__ sstep, uint32_t thr,
+                                                           float inv_keep, int wrows, int write_y) {
+  using frag = typename std::conditional<std::is_same<T, bf16>::value, bf16x8, fp16x8>::type;
+  constexpr int D = NK * 32;
+  constexpr int NKW = NK / 4;  // k-steps per wave
+  static_assert(NK % 4 == 0, "k-steps split over 4 waves");
+  __shared__ float red[4][16];
+  __shared__ float pred[4][16][33];
+  seed = mift_seed(seed, sstep);
+  const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * 16;
+  const int row = min(m0 + fr, M - 1);
+  const bool live = m0 + fr < M;
+  const int c00 = wave * NKW * 32 + g * 8;  // this lane's first column
+  const T* xr = x + (size_t)row * D + c00;
+  short8 xv[NKW];
+#pragma unroll
+  for (int s = 0; s < NKW; ++s) xv[s] = *reinterpret_cast<const short8*>(xr + s * 32);
+  T* yr = y + (size_t)row * D + c00;
+  // sum over the block's 4 waves of a per-row value held by lanes g = 0..3 of every wave
+  auto row_sum = [&](float v) {
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (g == 0) red[wave][fr] = v;
+    __syncthreads();
+    const float r = red[0][fr] + red[1][fr] + red[2][fr] + red[3][fr];
+    __syncthreads();  // red is reused by the next call
+    return r;
+  };
+  if constexpr (LN) {
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < NKW; ++s) {
+      float v[8];
+      unpack8<T>(xv[s], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += v[e];
+    }
+    const float mean = row_sum(sum) * (1.f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int s = 0; s < NKW; ++s) {
+      float v[8];
+      unpack8<T>(xv[s], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[e] - mean; q += d * d; }
+    }
+    const float rstd = rsqrtf(row_sum(q) * (1.f / D) + eps);
+#pragma unroll
+    for (int s = 0; s < NKW; ++s) {
+      const int c = c00 + s * 32;
+      float v[8], wv[8], bv[8];
+      unpack8<T>(xv[s], v);
+      load8<W>(lw + c, wv);
+      load8<W>(lb + c, bv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * rstd * wv[e] + bv[e];
+      short8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { T t = (T)v[e]; short h; __builtin_memcpy(&h, &t, 2); o[e] = h; }
+      xv[s] = o;  // the 16-bit y the consumer GEMM sees
+      if (live) *reinterpret_cast<short8*>(yr + s * 32) = o;
+    }
+    if (live && wave == 0 && g == 0) {
+      mean_out[m0 + fr] = mean;
+      rstd_out[m0 + fr] = rstd;
+    }
+  } else if (thr != 0) {  // residual-dropout backward: y = keep ? x/(1-p) : 0, stored and projected
+#pragma unroll
+    for (int s = 0; s < NKW; ++s) {
+      float v[8];
+      bool kp[8];
+      unpack8<T>(xv[s], v);
+      mift_keep8(seed, (uint64_t)row * D + c00 + s * 32, thr, kp);
+      short8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        T t = (T)(kp[e] ? v[e] * inv_keep : 0.f);
+        short h;
+        __builtin_memcpy(&h, &t, 2);
+        o[e] = h;
+      }
+      xv[s] = o;
+      if (live && write_y) *reinterpret_cast<short8*>(yr + s * 32) = o;
+    }
+  }
+  // projection partial over this wave's k-steps: acc[j] = y[16 rows] · pw[16j .. 16j+15]^T (rows
+  // >= wrows of pw are zero: not read)
+  const bool mask_in = LN && thr != 0;  // LoRA-input dropout of the LN output (scale folded in alpha)
+  const uint32_t hm0 = mift_hmix(seed, 0);
+  const bool hz = (uint64_t)M * D < (1ull << 33);
+  float4_ acc[NTI];
+#pragma unroll
+  for (int j = 0; j < NTI; ++j) acc[j] = float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NKW; ++s) {
+    const int c = c00 + s * 32;
+    short8 a = xv[s];
+    if (mask_in) {
+      uint32_t w[4], km[4];
+      __builtin_memcpy(w, &a, 16);
+      mift_andmask8(seed, hm0, hz, (uint64_t)row * D + c, thr, km);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] &= km[e];
+      __builtin_memcpy(&a, w, 16);
+    }
+    frag af;
+    __builtin_memcpy(&af, &a, 16);
+#pragma unroll
+    for (int j = 0; j < NTI; ++j) {
+      const int wr = j * 16 + fr;
+      const short8 b = wr < wrows ? *reinterpret_cast<const short8*>(pw + (size_t)wr * D + c)
+                                  : short8{0, 0, 0, 0, 0, 0, 0, 0};
+      frag bfv;
+      __builtin_memcpy(&bfv, &b, 16);
+      if constexpr (std::is_same<T, bf16>::value)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv, acc[j], 0, 0, 0);
+      else
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bfv, acc[j], 0, 0, 0);
+    }
+  }
+  // lane (fr, g) holds the partial out[4g + r][16j + fr]; sum the 4 waves' partials in LDS
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) pred[wave][4 * g + r][j * 16 + fr] = j < NTI ? acc[j < NTI ? j : 0][r] : 0.f;
+  __syncthreads();
+  for (int e = tid; e < 16 * 32; e += 256) {
+    const int r = e >> 5, c = e & 31;
+    if (m0 + r < M)
+      pout[(size_t)(m0 + r) * 32 + c] = (T)((pred[0][r][c] + pred[1][r][c] + pred[2][r][c] + pred[3][r][c]) * alpha);
+  }
+}
+
+// D = 32·NK with NK in {24, 32} (distilgpt2 / OPT-125m 768, 1024); false: use the row kernels
+inline bool rowproj_mfma_ok(int D) {
+  const char* e = getenv("MIFT_ROWPROJ_V");  // 1 = the row kernels (A/B knob, read per call)
+  return !(e && atoi(e) == 1) && (D == 768 || D == 1024);
+}
+
+template <typename F>
+void by_nk(int D, F&& f) {
+  if (D == 768) f(std::integral_constant<int, 24>{});
+  else f(std::integral_constant<int, 32>{});
+}
+
 template <int LR, typename F>
 void by_nit(int D, F&& f) {
   const int nit = (D + 255) / 256;
@@ -270,6 +438,26 @@ std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::
   const float inv = p > 0 ? mift_inv_keep(p) : 1.f;
   const bool wf32 = w.scalar_type() == at::kFloat;
   TORCH_CHECK(wf32 || w.scalar_type() == x.scalar_type(), "layer_norm_fwd_proj: LN weight dtype");
+  if (rowproj_mfma_ok(D)) {
+    auto go2 = [&](auto tt, auto wt) {
+      using T = decltype(tt);
+      using Wt = decltype(wt);
+      by_nk(D, [&](auto nk) {
+        constexpr int NK = decltype(nk)::value;
+        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, Wt, NK, 1, true> : rowproj_mfma_kernel<T, Wt, NK, 2, true>;
+        hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(),
+                           (const Wt*)w.data_ptr(), (const Wt*)b.data_ptr(), (T*)y.data_ptr(), mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, (float)eps,
+                           (float)alpha * inv, (uint64_t)seed, mift_seed_step(), thr, inv, (int)rank, 1);
+      });
+    };
+    if (x.scalar_type() == at::kBFloat16) {
+      if (wf32) go2(bf16{}, 0.f); else go2(bf16{}, bf16{});
+    } else {
+      if (wf32) go2(fp16{}, 0.f); else go2(fp16{}, fp16{});
+    }
+    return {y, mean, rstd, pout};
+  }
   auto go = [&](auto tt) {
     using T = decltype(tt);
     by_rank(rank, [&](auto lr) {
@@ -309,6 +497,22 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
   if (M == 0) return {y, pout};
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const float inv = p > 0 ? mift_inv_keep(p) : 1.f;
+  if (rowproj_mfma_ok(D)) {
+    auto go2 = [&](auto tt) {
+      using T = decltype(tt);
+      by_nk(D, [&](auto nk) {
+        constexpr int NK = decltype(nk)::value;
+        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, T, NK, 1, false> : rowproj_mfma_kernel<T, T, NK, 2, false>;
+        hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
+                           (const T*)nullptr, (T*)y.data_ptr(), (float*)nullptr, (float*)nullptr,
+                           (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, 0.f, (float)alpha, (uint64_t)seed,
+                           mift_seed_step(), thr, inv, (int)rank, thr != 0 ? 1 : 0);
+      });
+    };
+    if (x.scalar_type() == at::kBFloat16) go2(bf16{});
+    else go2(fp16{});
+    return {y, pout};
+  }
   auto go = [&](auto tt) {
     using T = decltype(tt);
     by_rank(rank, [&](auto lr) {

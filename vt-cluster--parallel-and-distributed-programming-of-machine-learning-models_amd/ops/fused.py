@@ -47,9 +47,15 @@ _LNPROJ_MAX_ROWS = int(os.environ.get("MIFT_LNPROJ_MAX_ROWS", "8"))
 _LNPROJ_MAX_D = int(os.environ.get("MIFT_LNPROJ_MAX_D", "1024"))
 
 
+def _rowproj_fused(D, rows):
+    """One fused row pass (LN / dropout-bwd + projection): the MFMA 16-row kernel at D in {768, 1024}
+    (any rank), the one-wave-per-row kernel for up to _LNPROJ_MAX_ROWS rows at other D <= 1024."""
+    return D in (768, 1024) or (rows <= _LNPROJ_MAX_ROWS and D <= _LNPROJ_MAX_D)
+
+
 def _ln_fwd_lora(x2, ln_w, ln_b, eps, lo, seed, training):
     """(LN(x), mean, rstd, T32 = s·dropout(LN(x))·Aᵀ) — fused row pass or LN + lora_proj."""
-    if lo.rows <= _LNPROJ_MAX_ROWS and x2.shape[-1] <= _LNPROJ_MAX_D:
+    if _rowproj_fused(x2.shape[-1], lo.rows):
         return K.layer_norm_fwd_proj(x2, ln_w, ln_b, eps, lo.A32s, lo.rows, 1.0, lo.p if training else 0.0, seed)
     a, mean, rstd = K.layer_norm_fwd(x2, ln_w, ln_b, eps)
     return a, mean, rstd, lo.forward(a, seed, training)
@@ -58,7 +64,7 @@ def _ln_fwd_lora(x2, ln_w, ln_b, eps, lo, seed, training):
 def _mask_proj(g2, p, seed, lo):
     """(gz = dropout-bwd(g), dT0 = dt_alpha·gz·B) — one row pass at small D; at OPT's D = 2560 the
     row pass (79 us) lost to mask_scale + the hipBLASLt projection (38 + 22 us)."""
-    if lo.rows <= _LNPROJ_MAX_ROWS and g2.shape[-1] <= _LNPROJ_MAX_D:
+    if _rowproj_fused(g2.shape[-1], lo.rows):
         return K.mask_proj(g2, p, seed, lo.B32t, lo.rows, lo.dt_alpha)
     gz = K.mask_scale(g2, p, seed) if p > 0 else g2
     return gz, K.lora_proj(gz, lo.B32t, lo.dt_alpha, 0.0, 0, rows=lo.rows)
