@@ -39,13 +39,32 @@ def _worker(rank, world, graph=False, steps=3, max_grad_norm=1e-3, bucket_mb=25.
                      step_log="none", save_steps=0, graph="on" if graph else "off", max_grad_norm=max_grad_norm)
     tr = Trainer(model, batcher, tc, ctx)
     names = [(n, o, p.numel()) for (n, p), o in zip(tr.arena.named, tr.arena.offsets)]
+    off2name = {o: n for n, o, _ in names}
+    events = []  # notification / launch order of the current step (last micro-step only counts)
+    red = tr.reducer
+    r_ready, r_launch = red._on_ready_offsets, red._launch
+
+    def on_ready(offsets):
+        events.append(("fused", [off2name.get(o, o) for o in offsets], red._sync))
+        r_ready(offsets)
+
+
+    def launch(b, where="finish"):
+        events.append(("LAUNCH", b["idx"], where))
+        r_launch(b, where)
+    red._on_ready_offsets = on_ready
+    tr.arena.grad_ready = on_ready
+    for n, p in tr.arena.named:  # the reducer's own hooks were bound at construction: log beside them
+        p.register_post_accumulate_grad_hook(lambda _p, n=n: events.append(("hook", n, red._sync)))
+    red._launch = launch
     recs = []
     real_step = tr.opt.step
 
     def hooked():
         (torch.cuda.synchronize() if torch.cuda.is_available() else None)
         recs.append({"grad": tr.arena.grad.detach().cpu().clone(),
-                     "log": list(tr.reducer.launch_log) if tr.reducer is not None else []})
+                     "log": [e for e in events if e[0] == "LAUNCH" or e[2]]})
+        events.clear()
         real_step()
         (torch.cuda.synchronize() if torch.cuda.is_available() else None)
         recs[-1]["param"] = tr.arena.param.detach().cpu().clone()
