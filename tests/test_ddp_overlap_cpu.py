@@ -117,3 +117,33 @@ def test_replica_checksum_is_exact():
     h = a.to(torch.bfloat16)
     assert replica_checksum([h]).shape == (1, 2)
     assert np.isfinite(replica_checksum([h]).numpy()).all()
+
+
+def test_fused_claim_counts_each_tensor_once():
+    """A tensor the fused forward claimed counts ONLY through the fused backward's notification:
+    PyTorch also runs its post-accumulate-grad hook (the Functions take the LoRA tensors as inputs),
+    and counting both launched the bucket half-way through backward — eager DP2 replicas diverged
+    from step 1 on the GPU (tools/diag_ddp_eager.py, round 3).  Unclaimed tensors (eager path) still
+    count through their hooks."""
+    from mift import lora as L
+    from mift.models import build_causal_lm
+    from mift.parallel.ddp import GradReducer
+    model = build_causal_lm("gpt2-tiny", seed=1)
+    L.inject(model, L.LoraConfig(r=4, lora_alpha=8, target_modules=["c_attn", "c_proj"]), seed=1)
+    arena = L.LoraArena(model)
+    red = GradReducer(arena, world=2, bucket_mb=1e9)  # one bucket holding every tensor
+    launches = []
+    red._launch = lambda b, where="finish": (launches.append(where), b.__setitem__("launched", True))
+    params = [p for _, p in arena.named]
+    half = len(arena.offsets) // 2
+    arena.grad_claim(arena.offsets[:half])  # the fused forward of the first half of the adapters
+    for p in params:  # every hook fires (as PyTorch does for the fused inputs too)
+        red._on_grad(p)
+    assert launches == []  # the claimed half has not been reported yet
+    arena.grad_ready(arena.offsets[:half - 1])
+    assert launches == []
+    arena.grad_ready(arena.offsets[half - 1:half])
+    assert launches == ["backward"]
+    red.finish = lambda: None
+    red.remove()
+    assert getattr(arena, "grad_claim", None) is None and getattr(arena, "grad_ready", None) is None

@@ -195,6 +195,153 @@ __global__ __launch_bounds__(256) void ln_wgrad_reduce_kernel(const float* __res
   db[c] = sb;
 }
 
+// ---- 16-B vector form (16-bit T, D % (8·LPR) == 0): RPW rows per wave, LPR = 64/RPW lanes per row,
+// 8 elements per lane per pass.  The 4-element form above issues 8-B loads and, at distilgpt2's
+// D = 768, three passes of one row per wave; ln_bwd read x, dy, w and dres that way at ~4.4 TB/s
+// (11.5-14.5 us per call at M = 8192).  Two rows per wave at D <= 1024 keep every lane busy with
+// whole 16-B pieces (D = 768: 32 lanes x 3 passes).  Same two-pass fp32 statistics.
+template <int LPR>
+MIFT_HD float lpr_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, typename W, int RPW, int NIT>
+__global__ __launch_bounds__(256) void ln_fwd8_kernel(const T* __restrict__ x, const W* __restrict__ w,
+                                                      const W* __restrict__ b, T* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int M, int D, float eps) {
+  constexpr int LPR = 64 / RPW;
+  const int lane = threadIdx.x & 63, l = lane % LPR;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= M) return;  // wave-uniform
+  const int row = min(row0 + lane / LPR, M - 1);
+  const bool live = row0 + lane / LPR < M;
+  const T* xr = x + (size_t)row * D + l * 8;
+  short8 xv[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) xv[it] = *reinterpret_cast<const short8*>(xr + it * LPR * 8);
+  float s = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    float v[8];
+    unpack8<T>(xv[it], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[e];
+  }
+  const float mean = lpr_sum<LPR>(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    float v[8];
+    unpack8<T>(xv[it], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = v[e] - mean; q += d * d; }
+  }
+  const float rstd = rsqrtf(lpr_sum<LPR>(q) / D + eps);
+  T* yr = y + (size_t)row * D + l * 8;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = (it * LPR + l) * 8;
+    float v[8], wv[8], bv[8];
+    unpack8<T>(xv[it], v);
+    load8<W>(w + c, wv);
+    load8<W>(b + c, bv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * rstd * wv[e] + bv[e];
+    if (live) store8<T>(yr + it * LPR * 8, v);
+  }
+  if (live && l == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) (+ dres),  g = dy * w
+template <typename T, typename W, int RPW, int NIT>
+__global__ __launch_bounds__(256) void ln_bwd8_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                      const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in, const T* __restrict__ dres,
+                                                      T* __restrict__ dx, int M, int D) {
+  constexpr int LPR = 64 / RPW;
+  const int lane = threadIdx.x & 63, l = lane % LPR;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= M) return;  // wave-uniform
+  const int row = min(row0 + lane / LPR, M - 1);
+  const bool live = row0 + lane / LPR < M;
+  const size_t base = (size_t)row * D + l * 8;
+  short8 xv[NIT], gv[NIT], rv[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    xv[it] = *reinterpret_cast<const short8*>(x + base + it * LPR * 8);
+    gv[it] = *reinterpret_cast<const short8*>(dy + base + it * LPR * 8);
+    if (dres != nullptr) rv[it] = *reinterpret_cast<const short8*>(dres + base + it * LPR * 8);
+  }
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = (it * LPR + l) * 8;
+    float xf[8], df[8], wv[8];
+    unpack8<T>(xv[it], xf);
+    unpack8<T>(gv[it], df);
+    load8<W>(w + c, wv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = df[e] * wv[e];
+      sg += g;
+      sgx += g * ((xf[e] - mean) * rstd);
+    }
+  }
+  sg = lpr_sum<LPR>(sg) / D;
+  sgx = lpr_sum<LPR>(sgx) / D;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = (it * LPR + l) * 8;
+    float xf[8], df[8], wv[8], o[8];
+    unpack8<T>(xv[it], xf);
+    unpack8<T>(gv[it], df);
+    load8<W>(w + c, wv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = rstd * (df[e] * wv[e] - sg - (xf[e] - mean) * rstd * sgx);
+    if (dres != nullptr) {
+      float r[8];
+      unpack8<T>(rv[it], r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += r[e];
+    }
+    if (live) store8<T>(dx + base + it * LPR * 8, o);
+  }
+}
+
+// (RPW, NIT) of the 16-B form for this D, or false (4-element form)
+inline bool ln8_shape(int D, int& rpw, int& nit) {
+  const char* e = getenv("MIFT_LN_V");  // 1 = the 4-element kernels (A/B knob, read per call)
+  if (e && atoi(e) == 1) return false;
+  rpw = D <= 1024 ? 2 : 1;
+  const int per = 8 * (64 / rpw);
+  if (D % per != 0) return false;
+  nit = D / per;
+  return nit == 1 || nit == 2 || nit == 3 || nit == 4 || nit == 5 || nit == 6 || nit == 8 || nit == 10;
+}
+
+inline bool a16(const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; }
+
+template <int RPW, typename F>
+void ln8_nit(int nit, F&& f) {
+  switch (nit) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    case 6: f(std::integral_constant<int, 6>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    default: f(std::integral_constant<int, 10>{}); break;  // ln8_shape admits no other value
+  }
+}
+
 template <typename T, typename W, int N>
 void ln_fwd_launch(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Tensor& y, at::Tensor& mean,
                    at::Tensor& rstd, int M, int D, float eps, hipStream_t st) {
@@ -207,6 +354,25 @@ void ln_fwd_launch(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
 template <typename T, typename W>
 void launch_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Tensor& y, at::Tensor& mean,
                 at::Tensor& rstd, int M, int D, float eps, hipStream_t st) {
+  if (M == 0) return;
+  int rpw8 = 0, nit8 = 0;
+  if constexpr (sizeof(T) == 2) {
+    if (ln8_shape(D, rpw8, nit8) && a16(x) && a16(w) && a16(b) && a16(y)) {
+      auto go = [&](auto rpwc) {
+        constexpr int RPW = decltype(rpwc)::value;
+        ln8_nit<RPW>(nit8, [&](auto nc) {
+          constexpr int NIT = decltype(nc)::value;
+          const int waves = (M + RPW - 1) / RPW;
+          ln_fwd8_kernel<T, W, RPW, NIT><<<(waves + 3) / 4, 256, 0, st>>>(
+              (const T*)x.data_ptr(), (const W*)w.data_ptr(), (const W*)b.data_ptr(), (T*)y.data_ptr(),
+              mean.data_ptr<float>(), rstd.data_ptr<float>(), M, D, eps);
+        });
+      };
+      if (rpw8 == 2) go(std::integral_constant<int, 2>{});
+      else go(std::integral_constant<int, 1>{});
+      return;
+    }
+  }
   int nit = (D + 255) / 256;
   if (nit <= 1) ln_fwd_launch<T, W, 1>(x, w, b, y, mean, rstd, M, D, eps, st);
   else if (nit <= 2) ln_fwd_launch<T, W, 2>(x, w, b, y, mean, rstd, M, D, eps, st);
@@ -241,6 +407,25 @@ void launch_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, 
                 const c10::optional<at::Tensor>& dbranch, const c10::optional<at::Tensor>& dw,
                 const c10::optional<at::Tensor>& db, int M, int D, uint64_t seed, uint32_t thr, float inv_keep,
                 hipStream_t st) {
+  if (M == 0) return;
+  int rpw8 = 0, nit8 = 0;
+  if constexpr (sizeof(T) == 2) {
+    if (!dbranch && ln8_shape(D, rpw8, nit8) && a16(dy) && a16(x) && a16(w) && a16(dx) && (!dres || a16(*dres))) {
+      auto go = [&](auto rpwc) {
+        constexpr int RPW = decltype(rpwc)::value;
+        ln8_nit<RPW>(nit8, [&](auto nc) {
+          constexpr int NIT = decltype(nc)::value;
+          const int waves = (M + RPW - 1) / RPW;
+          ln_bwd8_kernel<T, W, RPW, NIT><<<(waves + 3) / 4, 256, 0, st>>>(
+              (const T*)dy.data_ptr(), (const T*)x.data_ptr(), (const W*)w.data_ptr(), mean.data_ptr<float>(),
+              rstd.data_ptr<float>(), dres ? (const T*)dres->data_ptr() : nullptr, (T*)dx.data_ptr(), M, D);
+        });
+      };
+      if (rpw8 == 2) go(std::integral_constant<int, 2>{});
+      else go(std::integral_constant<int, 1>{});
+      return;
+    }
+  }
   int nit = (D + 255) / 256;
   if (nit <= 1) ln_bwd_launch<T, W, 1>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);
   else if (nit <= 2) ln_bwd_launch<T, W, 2>(dy, x, w, mean, rstd, dres, dx, dbranch, dw, db, M, D, seed, thr, inv_keep, st);

@@ -72,6 +72,19 @@ def _mask_proj(g2, p, seed, lo):
 _BWD = {0: 0, 1: 4, 2: 5, 3: 6}
 
 
+def _claim(arena, offsets):
+    """Tell the DP reducer, at forward time, that the fused backward writes these arena grads itself
+    and reports them through ``_notify``.  The Functions still take the LoRA tensors as autograd
+    inputs (so a block fed by the frozen embedding is still differentiated), and PyTorch runs their
+    post-accumulate-grad hooks although the backward returns None for them: counted as well, every
+    tensor would be "ready" twice and a bucket's all-reduce would launch before the last layers'
+    weight-grad kernels were queued (measured: eager DP2 replicas diverged from step 1,
+    tools/diag_ddp_eager.py)."""
+    cb = getattr(arena, "grad_claim", None)
+    if cb is not None:
+        cb(offsets)
+
+
 def _notify(arena, offsets):
     """Tell the DP reducer (mift.parallel.ddp) that these arena grads are final for this
     micro-step: the wgrad kernels are queued, so its bucket all-reduce can launch now and
@@ -167,6 +180,7 @@ class AdapterOps:
         self.arena = getattr(lin, "_arena", None)
         if self.arena is not None:
             self.offA, self.offB = lin._offA, lin._offB
+            _claim(self.arena, (self.offA, self.offB))
         if pk is not None and pk.dtype == dtype:
             pk.refresh()
             self.A32s, self.B32, self.B32t, self.At32 = lin._pack
@@ -242,6 +256,8 @@ class MultiAdapterOps:
         first = members[0][0]
         self.p = first.lora_dropout
         self.arena = getattr(first, "_arena", None)
+        if self.arena is not None:
+            _claim(self.arena, [o for l, _, _, _ in self.slots for o in (l._offA, l._offB)])
         key = (self.arena.version if self.arena is not None else None, dtype, _PACK_GEN[0])
         cached = getattr(cat, "_mpack", None)
         if self.arena is not None and cached is not None and cached[0] == key:

@@ -12,7 +12,10 @@ for LoRA on MI355X:
     ``finish()`` waits for all handles.  Readiness comes from two sources:
     the fused GPU blocks write LoRA grads straight into the arena and call
     ``arena.grad_ready(offsets)`` after queueing an adapter's wgrad kernels
-    (mift.ops.fused), the eager path from post-accumulate-grad hooks;
+    (mift.ops.fused), the eager path from post-accumulate-grad hooks.  A tensor
+    the fused forward claimed (``arena.grad_claim``) counts through the first
+    source only: PyTorch also runs its hook, and counting both launched buckets
+    before the last layers' grads existed (eager DP replicas diverged);
   * ``no_sync()`` for accumulation micro-steps (reference ``no_sync`` on
     steps 1..accum-1, verified in SURVEY C16);
   * default bucket 25 MB: distilgpt2 LoRA (1.6 MB fp32) and OPT-2.7B
@@ -59,12 +62,14 @@ class GradReducer:
             for p in b["params"]:
                 self._p2b[id(p)] = i
         self._off2p = {off: p for (_, p), off in named}
+        self._fused = set()  # ids of tensors whose grads the fused backward reports (hooks ignored)
         self._hooks = []
         self.launch_log = []  # (bucket index, "backward" | "finish") per launch of the last step
         if self.overlap:
             for _, p in arena.named:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
             arena.grad_ready = self._on_ready_offsets
+            arena.grad_claim = self._on_claim
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -94,7 +99,16 @@ class GradReducer:
             self._launch(b, "backward")
 
     def _on_grad(self, p):
+        if id(p) in self._fused:
+            return  # its readiness comes from the fused backward's notification (_on_ready_offsets)
         self._ready(p)
+
+    def _on_claim(self, offsets):
+        """Fused-forward claim: these arena slices are reported by ``_on_ready_offsets`` only."""
+        for off in offsets:
+            p = self._off2p.get(off)
+            if p is not None:
+                self._fused.add(id(p))
 
     def _on_ready_offsets(self, offsets):
         """Fused-backward notification: the arena slices at ``offsets`` hold this micro-step's grads."""
@@ -126,6 +140,8 @@ class GradReducer:
         self._hooks = []
         if getattr(self.arena, "grad_ready", None) == self._on_ready_offsets:
             self.arena.grad_ready = None
+        if getattr(self.arena, "grad_claim", None) == self._on_claim:
+            self.arena.grad_claim = None
 
 
 @torch.no_grad()
