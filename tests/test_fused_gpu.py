@@ -122,31 +122,37 @@ def test_opt_fused_matches_reference(dtype, p):
     lf = fused(input_ids=ids, attention_mask=mask, labels=ids, ignore_index=1, reduction="sum")["loss"]
     lf.backward()
     torch.testing.assert_close(lf.float(), lr.float(), rtol=2e-2, atol=1e-1)
-    # measured: fp16 1-4 %, bf16 3-9 % rel (ReLU-derivative flips of near-zero 16-bit pre-activations
-    # dominate; the error is the same with and without dropout, i.e. masks agree exactly)
+    # measured: fp16 1-4 %, bf16 3-9 % rel — 16-bit arithmetic itself (PyTorch's 16-bit eager path is
+    # as far from fp32: test_opt_fused_grads_as_accurate_as_torch_16bit); the same with and without
+    # dropout, i.e. the masks agree exactly
     _grad_close(ref, fused, 5e-2 if dtype == torch.float16 else 1.2e-1)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_opt_fused_grads_within_5pct_away_from_relu_kinks(dtype):
-    """The bf16 tolerance above (12 %) is ReLU-derivative flips: fc1 pre-activations within 16-bit
-    rounding of 0 take opposite branches in the fp32 reference and the bf16 kernels.  Push every
-    pre-activation away from the kink (fc1 bias = ±4, so |z| >> rounding) and the same comparison
-    holds within 5 % for bf16 too — the fused backward itself is as exact as fp16 (VERDICT r2 #8)."""
+def test_opt_fused_grads_as_accurate_as_torch_16bit(dtype):
+    """The fused-vs-fp32 gradient gap is 16-bit arithmetic itself, not a kernel defect: PyTorch's own
+    16-bit eager path on the same (rounded) weights — matmuls, SDPA, ReLU in bf16/fp16 — is as far
+    from the fp32 reference, and the fused kernels stay within 1.25x of it (+1 % absolute) on every
+    LoRA tensor.  The earlier "ReLU-kink flips" explanation did not hold: pushing fc1
+    pre-activations away from 0 (bias +-1/2/4, tools/diag_opt_relu.py) made the bf16 gap larger,
+    not smaller (6 % -> 21 % -> 69 % on layer-1 q/k), with no pre-activation near the kink — the gap
+    follows the attention-backward cancellation dS = P*(dP - D) at 16-bit P (VERDICT r2 #8)."""
     cfg, ref, fused = _opt_models(dtype, 0.0, lora_p=0.0)
-    with torch.no_grad():
-        for m_ in (ref, fused):
-            for n, q in m_.named_parameters():
-                if n.endswith("fc1.bias"):
-                    sgn = torch.where(torch.arange(q.numel(), device=q.device) % 2 == 0, 4.0, -4.0)
-                    q.copy_(sgn.to(q.dtype))
+    t16 = copy.deepcopy(fused)
+    t16.fused = False  # PyTorch 16-bit eager ops, same weights as the fused model
     torch.manual_seed(1)
     ids = torch.randint(3, cfg.vocab_size, (3, 96), device="cuda")
-    ref.train()
-    fused.train()
-    ref(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
-    fused(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
-    _grad_close(ref, fused, 5e-2)
+    for m_ in (ref, fused, t16):
+        m_.train()
+        m_(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
+    worst = []
+    for (n, p32), (_, pf), (_, pt) in zip(L.lora_parameters(ref), L.lora_parameters(fused), L.lora_parameters(t16)):
+        g = p32.grad.float()
+        ef = float((pf.grad.float() - g).norm() / (g.norm() + 1e-6))
+        et = float((pt.grad.float() - g).norm() / (g.norm() + 1e-6))
+        worst.append((ef, et, n))
+        assert ef <= 1.25 * et + 1e-2, f"{n}: fused rel err {ef:.3e} vs torch 16-bit {et:.3e}"
+    print(sorted(worst, reverse=True)[:3])
 
 
 def test_opt_arena_multi_adapter_matches_dense():

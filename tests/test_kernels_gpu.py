@@ -8,6 +8,11 @@ from mift.ops import reference as ref
 pytestmark = pytest.mark.gpu
 
 
+
+def _gnt(C, *args):
+    """gemm_nt with the epilogue projection off -> (out, preact)."""
+    return C.gemm_nt(*args, None, 32, 0.0, 0)[:2]
+
 def _C():
     assert mift.kernels_available(), f"extension not loaded: {mift._ext.error()!r}"
     import mift._C as C
@@ -44,7 +49,7 @@ def test_gemm_nt_plain(M, N, K):
     torch.manual_seed(1)
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
-    out = C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
+    out = _gnt(C, a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
     exp = a.float() @ b.float().t()
     torch.testing.assert_close(out.float(), exp, atol=3e-2, rtol=2e-2)
 
@@ -55,7 +60,7 @@ def test_gemm_nt_identity_asymmetric():
     n = 128
     a = torch.eye(n, device="cuda", dtype=torch.bfloat16)
     bm = (torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
-    out = C.gemm_nt(a, bm, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
+    out = _gnt(C, a, bm, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
     torch.testing.assert_close(out.float(), bm.float().t())
 
 
@@ -70,7 +75,7 @@ def test_gemm_nt_fused_epilogue(act):
     a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
     b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
     res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-    out, pre = C.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True, 1.0, None, 0, None, None, 0.0, 0)
+    out, pre = _gnt(C, a, b, bias, a2, b2, act, None, res, 0.1, 77, True, 1.0, None, 0, None, None, 0.0, 0)
     exp, exp_pre = ref.gemm_nt(a, b, bias, a2, b2, act, None, res, 0.1, 77, True)
     torch.testing.assert_close(pre.float(), exp_pre.float(), atol=5e-2, rtol=2e-2)
     torch.testing.assert_close(out.float(), exp.float(), atol=8e-2, rtol=3e-2)
@@ -84,7 +89,7 @@ def test_gemm_nt_act_backward(act):
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
     aux = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-    out = C.gemm_nt(a, b, None, None, None, act, aux, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
+    out = _gnt(C, a, b, None, None, None, act, aux, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)[0]
     exp, _ = ref.gemm_nt(a, b, None, None, None, act, aux)
     torch.testing.assert_close(out.float(), exp.float(), atol=5e-2, rtol=3e-2)
 
@@ -424,7 +429,7 @@ def test_gemm_ext_masked():
     b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
     a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
     b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
-    out = C.gemm_nt(a, b, None, a2, b2, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.05, 1234)[0]
+    out = _gnt(C, a, b, None, a2, b2, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.05, 1234)[0]
     exp = a.float() @ b.float().t() + ref.dropout(a2.float() @ b2.float().t(), 0.05, 1234)
     torch.testing.assert_close(out.float(), exp, atol=5e-2, rtol=3e-2)
 
@@ -443,10 +448,34 @@ def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):
     a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
     b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
     res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-    out, pre = C.gemm_nt(a, b, bias, a2, b2, 1, None, res, 0.1, 5, True, 1.0, None, tile, None, None, 0.0, 0)
+    out, pre = _gnt(C, a, b, bias, a2, b2, 1, None, res, 0.1, 5, True, 1.0, None, tile, None, None, 0.0, 0)
     exp, exp_pre = ref.gemm_nt(a, b, bias, a2, b2, 1, None, res, 0.1, 5, True)
     torch.testing.assert_close(pre.float(), exp_pre.float(), atol=5e-2, rtol=2e-2)
     torch.testing.assert_close(out.float(), exp.float(), atol=8e-2, rtol=3e-2)
     # repeated calls re-use the self-re-arming tile counters
-    out2 = C.gemm_nt(a, b, bias, a2, b2, 1, None, res, 0.1, 5, False, 1.0, None, tile, None, None, 0.0, 0)[0]
+    out2 = _gnt(C, a, b, bias, a2, b2, 1, None, res, 0.1, 5, False, 1.0, None, tile, None, None, 0.0, 0)[0]
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("tile", [0, 3, 7, 8, 9])
+@pytest.mark.parametrize("rows,p", [(8, 0.0), (8, 0.05), (24, 0.05)])
+def test_gemm_epilogue_projection_matches_lora_proj(tile, rows, p):
+    """T = drop(out)·pwᵀ from the GEMM epilogue (per column tile partials in fp32 slabs, summed in
+    order) == lora_proj over the stored output: same mask, fp32 sums, <= 16-bit rounding apart."""
+    C = _C()
+    torch.manual_seed(5)
+    M, K, N = 1000, 256, 768 if tile == 7 else 3072
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    bias = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    pw = torch.zeros(32, N, device="cuda", dtype=torch.bfloat16)
+    pw[:rows] = (0.05 * torch.randn(rows, N, device="cuda")).to(torch.bfloat16)
+    out, pre, t = C.gemm_nt(a, b, bias, None, None, 1, None, None, 0.0, 0, True, 1.0, None, tile, None, None, 0.0, 0,
+                            pw, rows, p, 4321)
+    out0, pre0 = _gnt(C, a, b, bias, None, None, 1, None, None, 0.0, 0, True, 1.0, None, tile, None, None, 0.0, 0)
+    assert torch.equal(out, out0) and torch.equal(pre, pre0)  # the projection leaves the GEMM output alone
+    exp = C.lora_proj(out, pw, 1.0, p, 4321, rows)
+    torch.testing.assert_close(t.float(), exp.float(), atol=2e-2, rtol=1e-2)
+    assert float(t[:, rows if rows > 16 else 16:].abs().max()) == 0.0
+    ref_t = ref.dropout(out.float(), p, 4321) @ pw.float().t()
+    torch.testing.assert_close(t.float(), ref_t, atol=5e-2, rtol=3e-2)

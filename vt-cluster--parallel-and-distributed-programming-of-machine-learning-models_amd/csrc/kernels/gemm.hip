@@ -75,6 +75,7 @@ struct LmArgs {
   int gpc;                // groups per split-K chunk
   float* partial;         // [S][M][N] fp32 split-K slabs
   int dbg;                // MIFT_LM_DBG (diagnostics only): bit 0 = skip the E store
+  int nt;                 // MIFT_LM_NT (A/B): bit 0 = nontemporal E stores (fwd), bit 1 = nt E loads (dgrad)
   int shift;              // > 0: labels are the UNSHIFTED [B*S] ids, S = shift (see lm_label)
 };
 
@@ -106,6 +107,17 @@ struct EpiArgs {
   const int64_t* sstep;    // device micro-step for graph-replayed dropout seeds (common.h mift_seed)
   int prefetch;            // epilogue: load aux / residual of all chunks up front (MIFT_EPI_PREFETCH=1; opt-in)
   int group_m;             // tile raster: 0 = row panels (n fastest); g > 0 = groups of g row panels, m fastest
+  // LoRA input projection of the OUTPUT (T = s·drop(out)·Aᵀ for the next layer's adapter, e.g. GPT-2
+  // mlp.c_proj's input f = gelu(c_fc(x))): pw = A32s [32, N] (s baked in), the first prow rows
+  // non-zero; each tile's partial over its BN columns goes to the fp32 slab pws [ntn][M][16|32]
+  // (deterministic), proj_reduce_kernel sums the slabs in order into pout [M, 32] x palpha.
+  const void* pw;
+  int prow;
+  uint32_t pthr;
+  uint64_t pseed;
+  float* pws;
+  void* pout;
+  float palpha;
 };
 
 // Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
@@ -208,6 +220,12 @@ struct CTile {
                                                        ((((c8 >> 2) ^ x) & ~1) << 2));
     return (x & 1) ? short8{v[4], v[5], v[6], v[7], v[0], v[1], v[2], v[3]} : v;
   }
+  // inverse of read8 (the half swap is an involution)
+  static MIFT_HD void write8(void* cs, int row, int c8, short8 v) {
+    const int x = sw(row);
+    *reinterpret_cast<short8*>(reinterpret_cast<short*>(cs) + row * CLD + ((((c8 >> 2) ^ x) & ~1) << 2)) =
+        (x & 1) ? short8{v[4], v[5], v[6], v[7], v[0], v[1], v[2], v[3]} : v;
+  }
 };
 
 template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, bool SKM, int EPI = 0>
@@ -229,6 +247,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   if (ep.sstep != nullptr) {
     ep.seed = mift_seed(ep.seed, ep.sstep);
     ep.ext_seed = mift_seed(ep.ext_seed, ep.sstep);
+    ep.pseed = mift_seed(ep.pseed, ep.sstep);
   }
 
   const int tid = threadIdx.x;
@@ -351,8 +370,11 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         const int i = 16 * h + wave + 8 * ii;
         const int r = i * 8 + srow;
         const int gr = min(r00 + r, rmax);
-        __builtin_amdgcn_global_load_lds((const void*)(G + (size_t)gr * ld + (kb + t) * BK + (spc ^ (r & 7)) * 8),
-                                         (void*)(base + i * 1024), 16, 0, 0);
+        const void* src = (const void*)(G + (size_t)gr * ld + (kb + t) * BK + (spc ^ (r & 7)) * 8);
+        if (EPI == 2 && o == 0 && (ep.lm.nt & 2))  // E is streamed once: keep W resident in L2
+          __builtin_amdgcn_global_load_lds(src, (void*)(base + i * 1024), 16, 0, 2);
+        else
+          __builtin_amdgcn_global_load_lds(src, (void*)(base + i * 1024), 16, 0, 0);
       }
     };
     const int arow = wm * WM + fr, brow = wn * WN + fr;
@@ -585,23 +607,78 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   #pragma unroll
         for (int e = 0; e < 8; ++e) z[e] += rv[e];
       }
+      if (ep.pws != nullptr) {  // the rounded output, in place of z, for the projection phase
+        short8 o;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) { T t = (T)z[e]; short h; __builtin_memcpy(&h, &t, 2); o[e] = h; }
+        CT::write8(Cs, row, c8, o);
+      }
       if (ep.lm.dbg & 1) return;  // diagnostics: MIFT_LM_DBG bit 0 skips the C store
       if (full) store8<T>(C + off, z);
       else for (int e = 0; e < N - gc; ++e) C[off + e] = (T)z[e];
     };
+    // ---- epilogue phase 3 (ep.pws): partial T = drop(out tile) · pw[:, n0 : n0+BN]ᵀ over this
+    // tile's columns, MFMA 16x16x32 from the C tile in LDS (read8 = one A fragment), one 16-row
+    // stripe per wave; the LoRA-input dropout mask of element (row, col) is the consumer's
+    // (index row·N + col, as lora_proj / lora_wgrad / the dgrad K-extension regenerate it).
+    auto proj_phase = [&]() {
+      __syncthreads();  // every chunk's output is in the C tile
+      const int fr = lane & 15, g = lane >> 4;
+      const uint32_t hm0 = mift_hmix(ep.pseed, 0);
+      const bool hz = (uint64_t)M * N < (1ull << 33);
+      const int PW = ep.prow <= 16 ? 16 : 32;
+      float* slab = ep.pws + (size_t)(n0 / BN) * M * PW;
+      for (int rt = wave; rt < BM / 16; rt += NW) {
+        const int row = rt * 16 + fr, gr = m0 + row;
+        float4_ pacc[2] = {float4_{0.f, 0.f, 0.f, 0.f}, float4_{0.f, 0.f, 0.f, 0.f}};
+  #pragma unroll
+        for (int s = 0; s < BN / 32; ++s) {
+          const int c = s * 32 + g * 8, gc = n0 + c;
+          short8 av = CT::read8(Cs, row, c);
+          if (gr >= M || gc >= N) av = short8{0, 0, 0, 0, 0, 0, 0, 0};
+          if (ep.pthr != 0) {
+            uint32_t w[4], km[4];
+            __builtin_memcpy(w, &av, 16);
+            mift_andmask8(ep.pseed, hm0, hz, (uint64_t)gr * N + gc, ep.pthr, km);
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] &= km[e];
+            __builtin_memcpy(&av, w, 16);
+          }
+          frag_t<T> af;
+          __builtin_memcpy(&af, &av, 16);
+  #pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (j * 16 >= ep.prow) break;  // uniform: rows >= prow of pw are zero
+            const int wr = j * 16 + fr;
+            const short8 bv = (wr < ep.prow && gc < N)
+                                  ? *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.pw) + (size_t)wr * N + gc)
+                                  : short8{0, 0, 0, 0, 0, 0, 0, 0};
+            frag_t<T> bf;
+            __builtin_memcpy(&bf, &bv, 16);
+            pacc[j] = mfma16<T>(bf, af, pacc[j]);  // lane: out[row fr][16j + 4g .. +3]
+          }
+        }
+        if (gr < M) {
+  #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            if (j * 16 < PW) *reinterpret_cast<float4_*>(slab + (size_t)gr * PW + j * 16 + 4 * g) = pacc[j];
+        }
+      }
+    };
     if constexpr (PF_OK) {
       if (!ep.prefetch) {
         for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{});
-        return;
-      }
-      short8 aux_r[ITER], res_r[ITER];
-      if (pf_aux) prefetch(ep.aux, aux_r);
-      if (pf_res) prefetch(ep.residual, res_r);
+      } else {
+        short8 aux_r[ITER], res_r[ITER];
+        if (pf_aux) prefetch(ep.aux, aux_r);
+        if (pf_res) prefetch(ep.residual, res_r);
   #pragma unroll
-      for (int it = 0; it < ITER; ++it) chunk(it, pf_aux, aux_r[it], pf_res, res_r[it]);
+        for (int it = 0; it < ITER; ++it) chunk(it, pf_aux, aux_r[it], pf_res, res_r[it]);
+      }
     } else {
       for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{});
     }
+    if (ep.pws != nullptr) proj_phase();
   };
 
   // ---- EPI 1: LM-head forward epilogue (see LmArgs).  The 16-bit E tile is staged in LDS
@@ -697,8 +774,11 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       const int v = tid + it * NT;
       const int r = v / VPR, c8 = (v % VPR) * 8;
       const int gr = m0 + r, gc = n0 + c8;
-      if (gr < M && gc < N)
-        *reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc) = CT::read8(Cs, r, c8);
+      if (gr < M && gc < N) {
+        const short8 ev = CT::read8(Cs, r, c8);
+        if (lm.nt & 1) __builtin_nontemporal_store(ev, reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc));
+        else *reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc) = ev;
+      }
     }
   };
 
@@ -902,6 +982,29 @@ int gemm_group_m(int N) {
   return N >= 8192 ? 4 : 0;
 }
 
+// out[m, 0:32] = alpha · Σ_t slab[t][m][0:PW] (columns >= PW zero): the per-column-tile partials of
+// the epilogue projection, summed in tile order (8 outputs per thread)
+template <typename T>
+__global__ __launch_bounds__(256) void proj_reduce_kernel(const float* __restrict__ slab, int ntn, int M, int PW,
+                                                          float alpha, T* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (row, 8-column group)
+  if (i >= (int64_t)M * 4) return;
+  const int m = (int)(i >> 2), c8 = (int)(i & 3) * 8;
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c8 < PW) {
+    for (int t = 0; t < ntn; ++t) {
+      const float* p = slab + ((size_t)t * M + m) * PW + c8;
+      const float4 a = *reinterpret_cast<const float4*>(p);
+      const float4 b = *reinterpret_cast<const float4*>(p + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= alpha;
+  store8<T>(out + (size_t)m * 32 + c8, v);
+}
+
 template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                  int K, const EpiArgs& ep, hipStream_t st) {
@@ -943,12 +1046,19 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
   }
   const int dp_tiles = nblk - sk_tiles;
   SkArgs sk{};
+  EpiArgs epx = ep;  // + the projection slab, sized by this tile's BN
+  at::Tensor slab;
+  const int ntn = (N + BN - 1) / BN, PW = ep.prow <= 16 ? 16 : 32;
+  if (ep.pw != nullptr) {
+    slab = at::empty({(int64_t)ntn * M * PW}, a.options().dtype(at::kFloat));
+    epx.pws = slab.data_ptr<float>();
+  }
   const T* A = (const T*)a.data_ptr();
   const T* Bp = (const T*)b.data_ptr();
   T* Cp = (T*)c.data_ptr();
   if (dp_tiles > 0)
     hipLaunchKernelGGL(kern, dim3(dp_tiles), dim3(NT), SMEM, st, A, Bp, Cp, a2, b2, M, N, K, (int)a.stride(0),
-                       (int)b.stride(0), (int)c.stride(0), ep, sk);
+                       (int)b.stride(0), (int)c.stride(0), epx, sk);
   if (sk_tiles > 0) {
     auto ws = at::empty({(int64_t)sk_tiles * S * BM * BN}, a.options().dtype(at::kFloat));
     sk.enabled = 1;
@@ -958,8 +1068,11 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
     sk.ws = ws.data_ptr<float>();
     sk.flags = sk_flags(sk_tiles);
     hipLaunchKernelGGL(kern_sk, dim3(sk_tiles * S), dim3(NT), SMEM, st, A, Bp, Cp, a2, b2, M, N, K, (int)a.stride(0),
-                       (int)b.stride(0), (int)c.stride(0), ep, sk);
+                       (int)b.stride(0), (int)c.stride(0), epx, sk);
   }
+  if (ep.pw != nullptr)
+    hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
+                       (const float*)epx.pws, ntn, M, PW, ep.palpha, (T*)ep.pout);
 }
 
 // Tile configurations (tile id -> geometry):
@@ -1098,6 +1211,7 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   ep.lm.ntn = ntn;
   ep.lm.shift = shift;
   if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);
+  if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   {
     const char* g = getenv("MIFT_GEMM_GROUP");  // row-panel order measured best for the fused head
     ep.group_m = g ? atoi(g) : 0;
@@ -1149,6 +1263,7 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   ep.lm.gpc = gpc;
   ep.lm.partial = partial.data_ptr<float>();
   ep.lm.shift = shift;
+  if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   SkArgs sk{};
   auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
   static bool attr = false;
@@ -1220,7 +1335,9 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                                      const c10::optional<at::Tensor>& residual, double dropout_p, int64_t seed,
                                      bool want_preact, double alpha, const c10::optional<at::Tensor>& out,
                                      int64_t tile, const c10::optional<at::Tensor>& alpha_t,
-                                     const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed) {
+                                     const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed,
+                                     const c10::optional<at::Tensor>& proj_w, int64_t proj_rows, double proj_p,
+                                     int64_t proj_seed) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm_nt: GPU tensors required");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_nt: 2-D operands");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_nt: K must be contiguous");
@@ -1290,7 +1407,21 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                 "gemm_nt: pre_add layout must match out");
     ep.pre_add = pre_add->data_ptr();
   }
-  if (M == 0 || N == 0) return {c, pre};
+  at::Tensor proj;
+  if (proj_w) {  // T = s·drop(out)·Aᵀ of the next adapter, from the epilogue (EpiArgs::pw)
+    TORCH_CHECK(proj_w->is_contiguous() && proj_w->size(0) == 32 && proj_w->size(1) == N &&
+                    proj_w->scalar_type() == a.scalar_type(),
+                "gemm_nt: proj_w must be [32, N] contiguous, same dtype");
+    TORCH_CHECK(proj_rows >= 1 && proj_rows <= 32 && N % 32 == 0, "gemm_nt: proj rows in [1, 32], N % 32 == 0");
+    proj = at::empty({M, 32}, a.options());
+    ep.pw = proj_w->data_ptr();
+    ep.prow = (int)proj_rows;
+    ep.pthr = mift_thr16(proj_p);
+    ep.pseed = (uint64_t)proj_seed;
+    ep.pout = proj.data_ptr();
+    ep.palpha = proj_p > 0 ? mift_inv_keep(proj_p) : 1.f;
+  }
+  if (M == 0 || N == 0) return {c, pre, proj};
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   if (a.scalar_type() == at::kBFloat16) {
     dispatch_tile<bf16>(a, b, c, a2 ? (const bf16*)a2->data_ptr() : nullptr, b2 ? (const bf16*)b2->data_ptr() : nullptr,
@@ -1301,5 +1432,5 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
   } else {
     TORCH_CHECK(false, "gemm_nt: bf16/fp16 only");
   }
-  return {c, pre};
+  return {c, pre, proj};
 }

@@ -72,6 +72,14 @@ def _mask_proj(g2, p, seed, lo):
 _BWD = {0: 0, 1: 4, 2: 5, 3: 6}
 
 
+def _epi_proj_kw(lo, seed, training):
+    """gemm kwargs that make the producing GEMM's epilogue emit ``lo.forward(out)`` (MIFT_EPI_PROJ=0:
+    the separate lora_proj pass, A/B knob read per call)."""
+    if lo is None or os.environ.get("MIFT_EPI_PROJ", "1") == "0":
+        return {}
+    return {"proj_w": lo.A32s, "proj_rows": lo.rows, "proj_p": lo.p if training else 0.0, "proj_seed": seed}
+
+
 def _claim(arena, offsets):
     """Tell the DP reducer, at forward time, that the fused backward writes these arena grads itself
     and reports them through ``_notify``.  The Functions still take the LoRA tensors as autograd
@@ -427,12 +435,18 @@ class MLP(torch.autograd.Function):
         else:
             a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
             T1 = None
+        # fc2's LoRA input projection T2 = s·drop(f)·A2ᵀ comes out of the fc1 epilogue (per column
+        # tile partials + one ordered reduction) instead of a lora_proj pass re-reading f
+        pk = _epi_proj_kw(lo2, seed_l2, training)
         if act == 2:  # ReLU: relu'(z) = [f > 0], so f doubles as the backward's aux (no pre-activation store)
-            f = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act)
+            r = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, **pk)
+            f, T2 = r if pk else (r, None)
             z = f
         else:
-            f, z = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, want_preact=True)
-        T2 = lo2.forward(f, seed_l2, training) if lo2 is not None else None
+            r = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, want_preact=True, **pk)
+            f, z, T2 = r if pk else r + (None,)
+        if lo2 is not None and T2 is None:
+            T2 = lo2.forward(f, seed_l2, training)
         pp = p if training else 0.0
         out = K.gemm(f, fc2.w_nk(), fc2.bias, T2, lo2.B32 if lo2 else None, residual=h2, dropout_p=pp, seed=seed)
         ctx.save_for_backward(h2, a, mean, rstd, ln_w, z, f, T1, T2)
