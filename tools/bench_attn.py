@@ -22,10 +22,17 @@ SHAPES = [("distilgpt2", 32, 256, 12, 64, torch.bfloat16, 0.1), ("distilgpt2-p0"
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--sweep", action="store_true",
+                    help="distilgpt2 shape over batch sizes (heads per CU: is the kernel per-CU-throughput or "
+                         "latency bound, and does the 1.5-heads-per-CU imbalance at B = 32 cost time?)")
     a = ap.parse_args()
     C = mift._ext.require()
     rows = []
-    for name, B, S, H, hd, dt, p in SHAPES:
+    shapes = SHAPES
+    if a.sweep:
+        shapes = [(f"distilgpt2-B{b}-p{p}", b, 256, 12, 64, torch.bfloat16, p) for p in (0.0, 0.1)
+                  for b in (8, 16, 21, 32, 43, 64)]
+    for name, B, S, H, hd, dt, p in shapes:
         qkv = torch.randn(B * S, 3 * H * hd, device="cuda", dtype=dt)
         sc = hd ** -0.5
         o, lse = C.attn_fwd(qkv, B, S, H, hd, sc, p, 1, None)

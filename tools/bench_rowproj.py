@@ -31,6 +31,7 @@ SHAPES = [  # (name, M, D, rank rows, dtype)
     ("dgpt.c_attn.ln_proj", 8192, 768, 8, torch.bfloat16),
     ("dgpt.c_fc.dT", 8192, 3072, 8, torch.bfloat16),
     ("opt125.qkv.ln_proj", 16384, 768, 28, torch.float16),
+    ("dgpt.c_attn.dT", 8192, 2304, 8, torch.bfloat16),
 ]
 
 
@@ -69,6 +70,11 @@ def main():
         row["lora_proj_p_us"] = round(t * 1e3, 1)
         t = timeit(lambda: K.lora_proj(x, w32, 1.0, 0.0, 0))
         row["lora_proj_us"] = round(t * 1e3, 1)
+        if D in (768, 1024, 2304):  # rowproj MFMA form by default; lora_proj's own kernel for A/B
+            os.environ["MIFT_ROWPROJ_V"] = "1"
+            t1 = timeit(lambda: K.lora_proj(x, w32, 1.0, 0.05, 7))
+            row["lora_proj_p_oldkernel_us"] = round(t1 * 1e3, 1)
+            os.environ.pop("MIFT_ROWPROJ_V")
         row["lora_proj_GBps"] = round(gb / (t * 1e-3), 0)
         t = timeit(lambda: torch.mm(x, w32.t()))
         row["torch_mm_us"] = round(t * 1e3, 1)

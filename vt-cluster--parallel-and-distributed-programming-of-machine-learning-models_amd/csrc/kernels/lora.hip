@@ -28,6 +28,10 @@
 #include <tuple>
 #include <vector>
 
+// rowproj.hip: the 4-wave 16-row MFMA projection, used for contiguous x at K in {768, 1024, 2304}
+bool mift_rowproj_lora_proj(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, double alpha, double p,
+                            int64_t seed, int64_t rows);
+
 namespace {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -565,6 +569,7 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   TORCH_CHECK(K % 32 == 0 && x.stride(0) % 8 == 0, "lora_proj: K % 32, aligned rows");
   auto out = at::empty({M, 32}, x.options());
   if (M == 0) return out;
+  if (mift_rowproj_lora_proj(x, w, out, alpha, p, seed, rows)) return out;  // rowproj.hip, MODE 2
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const uint32_t thr = mift_thr16(p);
   const float ik = p > 0 ? mift_inv_keep(p) : 1.f;

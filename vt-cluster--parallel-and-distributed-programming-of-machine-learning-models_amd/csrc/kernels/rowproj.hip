@@ -235,7 +235,10 @@ __global__ __launch_bounds__(256) void mask_proj_kernel(const T* __restrict__ x,
 // M = 8192 and ran 18.5 us against 7.1 us for the plain LN (latency-bound: one long chain per
 // wave).  Same numerics as the row kernels: y rounded to T before it is projected, dropped
 // elements zeroed (1/(1-p) folded into alpha by the host for LN), fp32 accumulation.
-template <typename T, typename W, int NK, int NTI, bool LN>
+// MODE: 0 = residual-dropout backward (y = keep·x/(1-p) stored and projected), 1 = LN (y = LN(x)
+// stored, LoRA-input dropout on the projection), 2 = plain LoRA projection (lora_proj semantics:
+// T = alpha·drop(x)·Wᵀ, nothing stored; replaces lora_proj's 16-row blocks at these widths).
+template <typename T, typename W, int NK, int NTI, int MODE>
 __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__ x, const W* __restrict__ lw,
                                                            const W* __restrict__ lb, T* __restrict__ y,
                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -271,6 +274,7 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
     __syncthreads();  // red is reused by the next call
     return r;
   };
+  constexpr bool LN = MODE == 1;
   if constexpr (LN) {
     float sum = 0.f;
 #pragma unroll
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
       mean_out[m0 + fr] = mean;
       rstd_out[m0 + fr] = rstd;
     }
-  } else if (thr != 0) {  // residual-dropout backward: y = keep ? x/(1-p) : 0, stored and projected
+  } else if (MODE == 0 && thr != 0) {  // residual-dropout backward: y = keep ? x/(1-p) : 0, stored and projected
 #pragma unroll
     for (int s = 0; s < NKW; ++s) {
       float v[8];
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
   }
   // projection partial over this wave's k-steps: acc[j] = y[16 rows] · pw[16j .. 16j+15]^T (rows
   // >= wrows of pw are zero: not read)
-  const bool mask_in = LN && thr != 0;  // LoRA-input dropout of the LN output (scale folded in alpha)
+  const bool mask_in = MODE != 0 && thr != 0;  // LoRA-input dropout (1/(1-p) folded into alpha by the host)
   const uint32_t hm0 = mift_hmix(seed, 0);
   const bool hz = (uint64_t)M * D < (1ull << 33);
   float4_ acc[NTI];
@@ -386,6 +390,15 @@ template <typename F>
 void by_nk(int D, F&& f) {
   if (D == 768) f(std::integral_constant<int, 24>{});
   else f(std::integral_constant<int, 32>{});
+}
+
+template <typename F>
+void by_nk_proj(int D, F&& f) {
+  switch (D) {
+    case 768: f(std::integral_constant<int, 24>{}); break;
+    case 1024: f(std::integral_constant<int, 32>{}); break;
+    default: f(std::integral_constant<int, 72>{}); break;  // 2304
+  }
 }
 
 template <int LR, typename F>
@@ -444,7 +457,7 @@ std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::
       using Wt = decltype(wt);
       by_nk(D, [&](auto nk) {
         constexpr int NK = decltype(nk)::value;
-        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, Wt, NK, 1, true> : rowproj_mfma_kernel<T, Wt, NK, 2, true>;
+        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, Wt, NK, 1, 1> : rowproj_mfma_kernel<T, Wt, NK, 2, 1>;
         hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(),
                            (const Wt*)w.data_ptr(), (const Wt*)b.data_ptr(), (T*)y.data_ptr(), mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, (float)eps,
@@ -502,7 +515,7 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
       using T = decltype(tt);
       by_nk(D, [&](auto nk) {
         constexpr int NK = decltype(nk)::value;
-        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, T, NK, 1, false> : rowproj_mfma_kernel<T, T, NK, 2, false>;
+        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, T, NK, 1, 0> : rowproj_mfma_kernel<T, T, NK, 2, 0>;
         hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
                            (const T*)nullptr, (T*)y.data_ptr(), (float*)nullptr, (float*)nullptr,
                            (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, 0.f, (float)alpha, (uint64_t)seed,
@@ -528,4 +541,36 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
   if (x.scalar_type() == at::kBFloat16) go(bf16{});
   else go(fp16{});
   return {y, pout};
+}
+
+// lora_proj on the 4-wave 16-row MFMA form (MODE 2) for contiguous x at K in {768, 1024, 2304}:
+// out = alpha·(1/(1-p))·drop(x)·wᵀ.  Returns false (caller runs lora_proj's own kernel) otherwise.
+// lora_proj's own kernel (16-row blocks, K split over the waves, 8 k-steps of loads in flight) ran
+// 8.5 / 20.2 us at M = 8192, K = 768 / 2304 against 6.4 / 18.2 here (profiles/r3/bench_rowproj_r3k.jsonl).
+bool mift_rowproj_lora_proj(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, double alpha, double p,
+                            int64_t seed, int64_t rows) {
+  const int M = x.size(0), K = x.size(1);
+  const char* e = getenv("MIFT_ROWPROJ_V");  // 1 = off (A/B knob, read per call)
+  // (K = 3072 measured slower here than lora_proj's kernel: 24.2 vs 21.9 us at M = 8192)
+  if ((e && atoi(e) == 1) || !(K == 768 || K == 1024 || K == 2304) || x.stride(0) != K ||
+      reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 != 0)
+    return false;
+  if (M == 0) return true;
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  const uint32_t thr = mift_thr16(p);
+  const float ik = p > 0 ? mift_inv_keep(p) : 1.f;
+  auto go = [&](auto tt) {
+    using T = decltype(tt);
+    by_nk_proj(K, [&](auto nk) {
+      constexpr int NK = decltype(nk)::value;
+      auto kern = rows <= 16 ? rowproj_mfma_kernel<T, T, NK, 1, 2> : rowproj_mfma_kernel<T, T, NK, 2, 2>;
+      hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
+                         (const T*)nullptr, (T*)nullptr, (float*)nullptr, (float*)nullptr, (const T*)w.data_ptr(),
+                         (T*)out.data_ptr(), M, 0.f, (float)alpha * ik, (uint64_t)seed, mift_seed_step(), thr, ik,
+                         (int)rows, 0);
+    });
+  };
+  if (x.scalar_type() == at::kBFloat16) go(bf16{});
+  else go(fp16{});
+  return true;
 }

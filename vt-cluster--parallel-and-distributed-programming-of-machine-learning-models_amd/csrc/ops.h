@@ -12,6 +12,10 @@ std::vector<at::Tensor> mift_layer_norm_bwd(const at::Tensor& dy, const at::Tens
                                             int64_t seed, bool want_wgrad);
 
 // ---- K1/K2 MFMA GEMM NT with fused epilogue (kernels/gemm.hip)
+// lora_proj on the rowproj.hip MFMA form when the shape fits (called by mift_lora_proj)
+bool mift_rowproj_lora_proj(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, double alpha, double p,
+                            int64_t seed, int64_t rows);
+
 std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
                                      const c10::optional<at::Tensor>& a2, const c10::optional<at::Tensor>& b2,
                                      int64_t act, const c10::optional<at::Tensor>& aux,
