@@ -208,6 +208,31 @@ def test_flash_attention_whole_sequence_kernels(S, p, dt, monkeypatch):
     torch.testing.assert_close(d_seq.float(), d_til.float(), atol=2e-3, rtol=2e-3)
 
 
+@pytest.mark.parametrize("B,S", [(32, 256), (24, 200), (40, 256)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_head_split_bit_identical(B, S, p, monkeypatch):
+    """C < B·H < 2C heads: the whole-sequence forward and dq kernels split 2C - B·H heads into two
+    query ranges (one full + one half head per CU).  Every query's arithmetic is unchanged, so
+    o, lse and dqkv equal the unsplit launch bit for bit (B = 40: 480 heads)."""
+    monkeypatch.setenv("MIFT_ATTN_SEQ", "1")
+    C = _C()
+    torch.manual_seed(3)
+    H, hd = 12, 64
+    qkv = torch.randn(B * S, 3 * H * hd, device="cuda").to(torch.bfloat16)
+    kvl = torch.randint(S // 2, S + 1, (B,), device="cuda", dtype=torch.int32)
+    out = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("MIFT_ATTN_SPLIT", split)
+        o, lse, bits = C.attn_fwd_bits(qkv, B, S, H, hd, hd ** -0.5, p, 5, kvl)
+        torch.manual_seed(4)
+        do = torch.randn_like(o)
+        d = C.attn_bwd_bits(do, qkv, o, lse, B, S, H, hd, hd ** -0.5, p, 5, kvl, bits if bits.numel() else None)
+        out[split] = (o, lse, bits, d)
+    # o, lse, dqkv (the keep-bit record's never-visited, non-causal entries are left unwritten)
+    for i, name in ((0, "o"), (1, "lse"), (3, "dqkv")):  # numerics vs fp32: test_flash_attention_*
+        assert torch.equal(out["1"][i], out["0"][i]), name
+
+
 @pytest.mark.parametrize("hd,S", [(64, 256), (64, 200), (32, 384), (80, 128), (128, 100)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_attention_keep_bits_match_hash(hd, S, dt, monkeypatch):

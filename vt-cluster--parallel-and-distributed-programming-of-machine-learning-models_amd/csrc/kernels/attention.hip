@@ -341,6 +341,75 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
 template <int HD>
 constexpr int seq_row_bytes() { return Geo<HD>::RS + Geo<HD>::TRS; }
 
+// Head split of the whole-sequence kernels (forward, dq).  Two blocks fit per CU (LDS), so with
+// C < B·H < 2C heads (distilgpt2: 384 over 256 CUs) half the CUs ran two heads and half one, and the
+// kernel took as long as a two-head CU.  The first nfull blocks take whole heads; each of the
+// remaining 2C - B·H heads is split into two blocks by causal work (query groups [0, gs) and
+// [gs, ng), gs balancing the 64-key tiles visited), so every CU gets one head and one half head
+// (blocks dispatch in index order: full heads fill the first slot of every CU, halves the second).
+// MIFT_ATTN_SPLIT=0 turns it off (A/B).
+int num_cus_attn() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+struct SeqSplit {
+  int nfull, gs;
+};
+MIFT_HD void seq_block(const SeqSplit& sp, int ng, int& bh, int& g0, int& g1) {
+  const int b = blockIdx.x;
+  if (b < sp.nfull) {
+    bh = b; g0 = 0; g1 = ng;
+  } else {
+    const int t = b - sp.nfull;
+    bh = sp.nfull + (t >> 1);
+    g0 = (t & 1) ? sp.gs : 0;
+    g1 = (t & 1) ? ng : sp.gs;
+  }
+}
+inline SeqSplit seq_split_plan(int BH, int S, int cus, int& blocks) {
+  SeqSplit sp{BH, 0};
+  blocks = BH;
+  const char* e = getenv("MIFT_ATTN_SPLIT");
+  const int ng = (S + 15) / 16;
+  if ((e && atoi(e) == 0) || BH <= cus || BH >= 2 * cus || ng < 4) return sp;
+  const int k = 2 * cus - BH;  // heads split in two
+  sp.nfull = BH - k;
+  long tot = 0;
+  for (int g = 0; g < ng; ++g) tot += (16 * g + 16 + BKV - 1) / BKV;
+  long acc = 0;
+  int gs = 1;
+  for (; gs < ng; ++gs) {
+    acc += (16 * (gs - 1) + 16 + BKV - 1) / BKV;
+    if (2 * acc >= tot) break;
+  }
+  sp.gs = gs;
+  blocks = BH + k;
+  return sp;
+}
+// dK/dV: key groups [0, gs) and [gs, ng); a key group visits the 64-query tiles from its own to
+// the last, so the weights run the other way
+inline SeqSplit seq_split_plan_kv(int BH, int S, int cus, int& blocks) {
+  SeqSplit sp = seq_split_plan(BH, S, cus, blocks);
+  if (sp.nfull == BH) return sp;
+  const int ng = (S + 15) / 16, nqt = (S + BQ - 1) / BQ;
+  long tot = 0;
+  for (int g = 0; g < ng; ++g) tot += nqt - (16 * g) / BQ;
+  long acc = 0;
+  int gs = 1;
+  for (; gs < ng; ++gs) {
+    acc += nqt - (16 * (gs - 1)) / BQ;
+    if (2 * acc >= tot) break;
+  }
+  sp.gs = gs;
+  return sp;
+}
+
 // MIFT_ATTN_SEQ: 0 = tiled kernels only, 1 = whole-sequence kernels when they fit and there are
 // >= 256 heads to fill the chip (default), 2 = whenever they fit (tests, A/B); read per call
 int attn_seq_mode() {
@@ -353,7 +422,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
                                                               float* __restrict__ lse, const int* __restrict__ kv_len,
                                                               int B, int S, int H, float scale, uint64_t seed,
                                                               const int64_t* __restrict__ sstep, uint32_t thr,
-                                                              float inv_keep, uint16_t* __restrict__ dmask) {
+                                                              float inv_keep, uint16_t* __restrict__ dmask,
+                                                              SeqSplit split) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   constexpr int NT = NW * 64;
@@ -365,7 +435,9 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, qc = lane & 15;
-  const int bh = blockIdx.x;
+  int bh, g0, g1;
+  seq_block(split, (S + 15) / 16, bh, g0, g1);
+  const int SPB = min(SP, (16 * g1 + BKV - 1) / BKV * BKV);  // keys this block's queries can see
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
@@ -378,19 +450,19 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
   const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
   const uint32_t hm0 = mift_hmix(seed, 0);
 
-  const int ng = (S + 15) / 16;
+  const int ng = g1;  // query groups [g0, g1) of this block (the whole head unless split)
   // Q fragments of this wave's first two 16-query groups are requested before K/V are staged, so
   // their latency hides under the staging instead of stalling each group's first MFMA
   vec8<T> qpre[2][G::NKS];
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl) {
-    const int grp = (sl & 1) ? (sl + 1) * NW - 1 - wave : sl * NW + wave;
+    const int grp = g0 + ((sl & 1) ? (sl + 1) * NW - 1 - wave : sl * NW + wave);
     if (grp < ng) load_reg_frags<T, HD>(qpre[sl], Qg, ld, grp * 16 + qc, S, lane);
   }
-  // ---- stage K and V of the whole sequence: 8 chunks in flight per thread per round
+  // ---- stage K and V of the keys visible to this block: 8 chunks in flight per thread per round
   {
     constexpr int U = 4;
-    const int nch = SP * G::CH;
+    const int nch = SPB * G::CH;
     for (int c0 = tid; c0 < nch; c0 += U * NT) {
       short8 kv[U], vv[U];
 #pragma unroll
@@ -417,7 +489,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
     }
     if (G::HDP != HD) {
       constexpr int PADC = (G::HDP - HD) / 8;
-      for (int i = tid; i < SP * PADC; i += NT) {
+      for (int i = tid; i < SPB * PADC; i += NT) {
         const int r = i / PADC, c = HD / 8 + i % PADC;
         *reinterpret_cast<short8*>(Ks + r * G::RS + c * 16) = short8{0, 0, 0, 0, 0, 0, 0, 0};
       }
@@ -427,8 +499,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
 
   T* Og = out + (int64_t)b * S * D + h * HD;
   for (int slot = 0;; ++slot) {
-    const int grp = (slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave;  // snake order
-    if (slot * NW >= ng) break;
+    const int grp = g0 + ((slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave);  // snake order
+    if (slot * NW >= ng - g0) break;
     if (grp >= ng) continue;
     const int q0 = grp * 16, myq = q0 + qc;
     vec8<T> qf[G::NKS];
@@ -850,7 +922,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
                                                                  const int* __restrict__ kv_len, int B, int S, int H,
                                                                  float scale, uint64_t seed,
                                                                  const int64_t* __restrict__ sstep, uint32_t thr,
-                                                                 float inv_keep, const uint16_t* __restrict__ dmask) {
+                                                                 float inv_keep, const uint16_t* __restrict__ dmask,
+                                                                 SeqSplit split) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   constexpr int NT = NW * 64;
@@ -863,7 +936,9 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, qc = lane & 15;
-  const int bh = blockIdx.x;
+  int bh, g0, g1;
+  seq_block(split, (S + 15) / 16, bh, g0, g1);
+  const int SPB = min(SP, (16 * g1 + BKV - 1) / BKV * BKV);  // keys this block's queries can see
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
@@ -877,16 +952,18 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
   const float c2 = scale * LOG2E;
   const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
   const uint32_t hm0 = mift_hmix(seed, 0);
-  const int ng = (S + 15) / 16;
-  stage_rows<T, HD>(Ks, Kg, ld, S, SP, tid, NT);
-  stage_rows<T, HD>(Vs, Vg, ld, S, SP, tid, NT);
+  const int ng = g1;  // query groups [g0, g1) of this block (the whole head unless split)
+  stage_rows<T, HD>(Ks, Kg, ld, S, SPB, tid, NT);
+  stage_rows<T, HD>(Vs, Vg, ld, S, SPB, tid, NT);
   // keep-bit records of the forward (KEEP BITS): query q's record goes to the row-q padding, 8-B
-  // words 0..3 (64-key tiles 0..3) in the K image, 4..7 in the V image
+  // words 0..3 (64-key tiles 0..3) in the K image, 4..7 in the V image (this block's queries only;
+  // the records keep the full-head width NW4 = SP / 64)
   const int NW4 = SP / 64;
   const bool mk = dmask != nullptr;
   if (mk) {
     MIFT_ASSERT(NW4 <= 8);
-    for (int i = tid; i < S * NW4; i += NT) {
+    const int qa = 16 * g0, qb = min(S, 16 * g1);
+    for (int i = qa * NW4 + tid; i < qb * NW4; i += NT) {
       const int q = i / NW4, w = i % NW4;
       const uint2 v = *reinterpret_cast<const uint2*>(dmask + ((int64_t)bh * S + q) * (NW4 * 4) + w * 4);
       *reinterpret_cast<uint2*>((w < 4 ? Ks : Vs) + (size_t)q * G::RS + PADOFF + (w & 3) * 8) = v;
@@ -895,8 +972,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
   __syncthreads();
   T* dQg = dqkv + (int64_t)b * S * ld + h * HD;
   for (int slot = 0;; ++slot) {
-    const int grp = (slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave;
-    if (slot * NW >= ng) break;
+    const int grp = g0 + ((slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave);
+    if (slot * NW >= ng - g0) break;
     if (grp >= ng) continue;
     const int q0 = grp * 16, myq = q0 + qc;
     vec8<T> qf[G::NKS], df[G::NKS];
@@ -979,7 +1056,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
                                                                    const int* __restrict__ kv_len, int B, int S, int H,
                                                                    float scale, uint64_t seed,
                                                                    const int64_t* __restrict__ sstep, uint32_t thr,
-                                                                   float inv_keep, const uint16_t* __restrict__ dmask) {
+                                                                   float inv_keep, const uint16_t* __restrict__ dmask,
+                                                                   SeqSplit split) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   constexpr int NT = NW * 64;
@@ -1000,7 +1078,9 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, kc = lane & 15;
-  const int bh = blockIdx.x;
+  int bh, g0, g1;
+  seq_block(split, (S + 15) / 16, bh, g0, g1);  // key groups [g0, g1) of head bh
+  const int QA = (16 * g0) / BQ * BQ;            // first query row any of them visits (causal)
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
@@ -1011,10 +1091,11 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
   const int klen = kv_len ? kv_len[b] : S;
   MIFT_ASSERT(klen >= 0 && klen <= S);
   const float c2 = scale * LOG2E;
-  const int ng = (S + 15) / 16;
-  stage_rows<T, HD>(Qs, Qg, ld, S, SP, tid, NT);
-  stage_rows<T, HD>(dOs, dOg, D, S, SP, tid, NT);
-  for (int i = tid; i < SP; i += NT) {
+  const int ng = g1;
+  // rows [QA, SP) of the Q / dO images (stage_rows from the offset row keeps the image row = query)
+  stage_rows<T, HD>(Qs + (size_t)QA * G::RS, Qg + (int64_t)QA * ld, ld, S - QA, SP - QA, tid, NT);
+  stage_rows<T, HD>(dOs + (size_t)QA * G::RS, dOg + (int64_t)QA * D, D, S - QA, SP - QA, tid, NT);
+  for (int i = QA + tid; i < SP; i += NT) {
     const int q = min(i, S - 1);
     *reinterpret_cast<float*>(pad(Qs, i, 0)) = lse[(int64_t)bh * S + q] * LOG2E;
     *reinterpret_cast<float*>(pad(dOs, i, 0)) = Dv[(int64_t)bh * S + q];
@@ -1026,7 +1107,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
   auto rec_at = [&](int q, int e) -> char* { return e < 14 ? pad(Qs, q, 4 + e * 2) : pad(dOs, q, 4 + (e - 14) * 2); };
   if (mk) {
     MIFT_ASSERT(NR <= 28);
-    for (int i = tid; i < S * (NR / 4); i += NT) {
+    for (int i = QA * (NR / 4) + tid; i < S * (NR / 4); i += NT) {
       const int q = i / (NR / 4), w = i % (NR / 4);
       const uint2 v = *reinterpret_cast<const uint2*>(dmask + ((int64_t)bh * S + q) * NR + w * 4);
 #pragma unroll
@@ -1040,8 +1121,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
   const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
   const uint32_t hm0 = mift_hmix(seed, 0);
   for (int slot = 0;; ++slot) {
-    const int grp = (slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave;
-    if (slot * NW >= ng) break;
+    const int grp = g0 + ((slot & 1) ? (slot + 1) * NW - 1 - wave : slot * NW + wave);
+    if (slot * NW >= ng - g0) break;
     if (grp >= ng) continue;
     const int k0 = grp * 16, mykey = k0 + kc;
     vec8<T> kf[G::NKS], vf[G::NKS];
@@ -1430,9 +1511,11 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       attr = true;
     }
-    hipLaunchKernelGGL(kern, dim3(B * H), dim3(512), seq_smem, st, (const T*)qkv.data_ptr(), (T*)o.data_ptr(),
+    int nblk = B * H;
+    const SeqSplit split = seq_split_plan(B * H, S, num_cus_attn(), nblk);
+    hipLaunchKernelGGL(kern, dim3(nblk), dim3(512), seq_smem, st, (const T*)qkv.data_ptr(), (T*)o.data_ptr(),
                        lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep,
-                       thr != 0 ? dmask : nullptr);
+                       thr != 0 ? dmask : nullptr, split);
     return;
   }
   if (qg == 2) {
@@ -1465,12 +1548,16 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
       (void)hipFuncSetAttribute((const void*)kk, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       attr = true;
     }
-    hipLaunchKernelGGL(kq, dim3(B * H), dim3(512), seq_dq, st, (const T*)qkv.data_ptr(), (const T*)o.data_ptr(),
+    int nblk = B * H;
+    const SeqSplit split = seq_split_plan(B * H, S, num_cus_attn(), nblk);
+    hipLaunchKernelGGL(kq, dim3(nblk), dim3(512), seq_dq, st, (const T*)qkv.data_ptr(), (const T*)o.data_ptr(),
                        (const T*)dout.data_ptr(), lse.data_ptr<float>(), Dv.data_ptr<float>(), (T*)dqkv.data_ptr(),
-                       kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep, thr != 0 ? dmask : nullptr);
-    hipLaunchKernelGGL(kk, dim3(B * H), dim3(512), seq_kv, st, (const T*)qkv.data_ptr(), (const T*)dout.data_ptr(),
+                       kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep, thr != 0 ? dmask : nullptr, split);
+    int nblk_kv = B * H;
+    const SeqSplit split_kv = seq_split_plan_kv(B * H, S, num_cus_attn(), nblk_kv);
+    hipLaunchKernelGGL(kk, dim3(nblk_kv), dim3(512), seq_kv, st, (const T*)qkv.data_ptr(), (const T*)dout.data_ptr(),
                        lse.data_ptr<float>(), Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed,
-                       mift_seed_step(), thr, inv_keep, thr != 0 ? dmask : nullptr);
+                       mift_seed_step(), thr, inv_keep, thr != 0 ? dmask : nullptr, split_kv);
     return;
   }
   const int nqt = (S + BQ - 1) / BQ, nkt = (S + BKV - 1) / BKV;
