@@ -394,6 +394,37 @@ def test_lora_wgrad_group_deterministic(det, monkeypatch):
         assert torch.equal(o, outs[0]), "deterministic wgrad must be bit-reproducible"
 
 
+@pytest.mark.parametrize("qoff,rank", [(0, 8), (8, 16)])
+def test_lora_wgrad_in_kernel_reduction_matches_separate_launch(qoff, rank, monkeypatch):
+    """Opt-in MIFT_WGRAD_FIN=1: the last chunk block of every column tile reduces its slabs in chunk
+    order (one launch); the default separate reduction launch adds the same slabs in the same order: equal bits,
+    over a grouped launch of dB (mode 1) and multi-slot dA (mode 2) problems; repeated launches keep
+    the self-re-arming tile counters consistent."""
+    C = _C()
+    torch.manual_seed(6)
+    M = 8192
+    xs = [torch.randn(M, P, device="cuda", dtype=torch.bfloat16) for P in (2304, 768, 3072)]
+    ys = [torch.randn(M, 32, device="cuda", dtype=torch.bfloat16) for _ in xs]
+    n = 64 + sum(rank * x.shape[1] for x in xs) + 4096
+    offs, o = [], 64
+    for x in xs:
+        offs.append(o)
+        o += rank * x.shape[1]
+    meta = []
+    for i, x in enumerate(xs):
+        meta += [1 if i != 1 else 2, 1, qoff, rank, offs[i]] + [0, 0, 0] * 3 + [11 + i]
+    res = {}
+    for fin in ("1", "0", "1"):
+        monkeypatch.setenv("MIFT_WGRAD_FIN", fin)
+        arena = torch.full((n,), 0.5, device="cuda")
+        C.lora_wgrad_group(arena, xs, ys, meta, [0.0, 0.05, 0.0])
+        res.setdefault(fin, []).append(arena)
+    assert torch.equal(res["1"][0], res["0"][0]) and torch.equal(res["1"][1], res["0"][0])
+    exp = (xs[0].float().t() @ ys[0].float()[:, qoff:qoff + rank]).reshape(-1) + 0.5  # dB layout [P, rank]
+    got = res["1"][0][offs[0]:offs[0] + rank * xs[0].shape[1]]
+    assert ((got - exp).norm() / exp.norm()).item() < 1e-2
+
+
 def test_grad_stats_deterministic():
     """grad_stats run 100x on the same arena gives one bit pattern (per-block partials + one
     fixed-order reduction block, no float atomics), close to the fp64 sum; non-finite count exact."""

@@ -228,6 +228,8 @@ struct WgProb {
 struct WgArgs {
   float* out;
   float* ws;        // deterministic mode: [blocks][NQT*16][64] fp32 partial slabs (nullptr: atomics)
+  int* flags;       // per column tile arrival counters (zero, self-re-arming): the last chunk block of a
+                    // tile reduces its slabs in chunk order (nullptr: separate lora_wgrad_reduce launch)
   const int64_t* sstep;
   int np;
   WgProb p[WG_MAXP];
@@ -265,6 +267,9 @@ MIFT_HD void wg_store(const WgArgs& args, const WgProb& pr, const float4_ (&acc)
       }
     }
 }
+
+template <int NQT>
+MIFT_HD void wg_reduce_tile(const WgArgs& args, const WgProb& pr, int pt);
 
 template <typename T>
 __global__ __launch_bounds__(256) void lora_wgrad_kernel(const WgArgs args) {
@@ -510,19 +515,33 @@ __global__ __launch_bounds__(256) void lora_wgrad2_kernel(const WgArgs args) {
     for (int c = 0; c < NQT; ++c) acc[c] *= inv_keep;
   }
   wg_store<NQT>(args, pr, acc, p0, wave, g, li);
+  if (args.flags != nullptr) {  // the last chunk block of this column tile reduces its slabs
+    __shared__ int last;
+    __threadfence();  // this block's slab stores are visible device-wide before it arrives
+    __syncthreads();
+    if (tid == 0) {
+      const int nch = (M + rows_per_block - 1) / rows_per_block;
+      int* f = args.flags + pr.tile0 + pt;
+      const int prev = __hip_atomic_fetch_add(f, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == nch - 1;
+      if (last) __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    __syncthreads();
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other chunks' slabs
+      wg_reduce_tile<NQT>(args, pr, pt);
+    }
+  }
 }
 
 // Deterministic reduction: block t = column tile t of the launch (problem pi, tile pt) sums the
 // row-chunk slabs of that tile in chunk order and adds the result to the output — each output
 // element is owned by exactly one thread (the host checks that the problems' slots are disjoint).
+// Sum the chunk slabs of column tile pt of problem pr in chunk order and add the result into the
+// output (one thread per 4 slab elements of each 16-column group).
 template <int NQT>
-__global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const WgArgs args) {
-  int pi = 0;
-#pragma unroll 1
-  while (pi + 1 < args.np && (int)blockIdx.x >= args.p[pi + 1].tile0) ++pi;
-  const WgProb& pr = args.p[pi];
+MIFT_HD void wg_reduce_tile(const WgArgs& args, const WgProb& pr, int pt) {
   const int ntp = pr.P / 64;
-  const int pt = blockIdx.x - pr.tile0;
   const int nch = (pr.M + pr.rows - 1) / pr.rows;
   constexpr int SL = NQT * 16 * 64;
 #pragma unroll
@@ -555,6 +574,14 @@ __global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const WgArgs arg
       }
     }
   }
+}
+
+template <int NQT>
+__global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const WgArgs args) {
+  int pi = 0;
+#pragma unroll 1
+  while (pi + 1 < args.np && (int)blockIdx.x >= args.p[pi + 1].tile0) ++pi;
+  wg_reduce_tile<NQT>(args, args.p[pi], blockIdx.x - args.p[pi].tile0);
 }
 
 }  // namespace
@@ -621,6 +648,15 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
 }
 
 namespace {
+// persistent per-column-tile arrival counters of the in-kernel slab reduction (zeroed once; every
+// finisher re-arms its own; first allocated by an eager call, outside any hipGraph capture)
+int* wg_flags(int n) {
+  static at::Tensor flags;
+  if (!flags.defined() || flags.numel() < n)
+    flags = at::zeros({std::max<int64_t>(n, 1 << 14)}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA));
+  return flags.data_ptr<int>();
+}
+
 template <typename T>
 void launch_wgrad(WgArgs& args, hipStream_t st) {
   // rows per block: ~2048 blocks over the group (eight per CU: loads of several blocks in flight
@@ -656,13 +692,22 @@ void launch_wgrad(WgArgs& args, hipStream_t st) {
       args.p[i].tile0 = tiles;
       tiles += args.p[i].P / 64;
     }
+    // MIFT_WGRAD_FIN=1 (opt-in, measured much slower): the last chunk block of every column tile
+    // reduces in place instead of a second launch.  Every block then needs an agent-scope release
+    // (its slab visible to the finisher on another XCD), which on the multi-XCD MI355X writes back
+    // the XCD's L2: the distilgpt2 step went 5.09 -> 6.74 ms (profiles/r3/step_ab_wgrad_finisher_rejected.jsonl).
+    const char* fe = getenv("MIFT_WGRAD_FIN");
+    const bool fin = !v1 && fe && atoi(fe) == 1;
+    args.flags = fin ? wg_flags(tiles) : nullptr;
     if (v1) lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
     else if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
     else lora_wgrad2_kernel<T, 2><<<blk, 256, 0, st>>>(args);
+    if (fin) return;
     if (nqt == 1) lora_wgrad_reduce_kernel<1><<<tiles, 256, 0, st>>>(args);
     else lora_wgrad_reduce_kernel<2><<<tiles, 256, 0, st>>>(args);
     return;
   }
+  args.flags = nullptr;
   args.ws = nullptr;
   if (v1) lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
   else if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
