@@ -490,7 +490,7 @@ def test_gemm_ext_masked():
     torch.testing.assert_close(out.float(), exp, atol=5e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("M,N,K", [(4096, 2560, 2560), (1000, 2304, 768), (8192, 768, 3072), (777, 1000, 320),
                                    (300, 520, 64)])
 def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):
@@ -513,7 +513,7 @@ def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):
     assert torch.equal(out, out2)
 
 
-@pytest.mark.parametrize("tile", [0, 3, 7, 8, 9, 10])
+@pytest.mark.parametrize("tile", [0, 3, 7, 8, 9])
 @pytest.mark.parametrize("rows,p", [(8, 0.0), (8, 0.05), (24, 0.05)])
 def test_gemm_epilogue_projection_matches_lora_proj(tile, rows, p):
     """T = drop(out)·pwᵀ from the GEMM epilogue (per column tile partials in fp32 slabs, summed in

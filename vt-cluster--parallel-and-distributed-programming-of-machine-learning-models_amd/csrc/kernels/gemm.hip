@@ -163,41 +163,6 @@ MIFT_HD float4_ mfma16(frag_t<T> a, frag_t<T> b, float4_ c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// LDS byte address of a pointer into the dynamic shared segment
-MIFT_HD uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
-}
-// 16-B LDS read issued in program order; the caller waits (s_waitcnt lgkmcnt) before any use
-template <int OFF, typename F>
-MIFT_HD void lds_rd(F& dst, uint32_t addr) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
-}
-// acc += b·a with the accumulator pinned to AGPRs (the wide-wave loop's 256 accumulators: the
-// builtin form lets the register allocator shuttle ~370 accumulator copies per k-tile between the
-// VGPR and AGPR files, and spill).  The compiler sees an opaque instruction here, so the hazard
-// waits between MFMA results and their other readers are explicit (mfma_fence).
-// The asm is volatile: the wide-wave loop orders its MFMAs, LDS reads and waits by hand.
-template <typename T>
-MIFT_HD void mfma16_acc(float4_& c, frag_t<T> b, frag_t<T> a) {
-  if constexpr (std::is_same<T, bf16>::value)
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
-  else
-    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
-}
-// >= 32 wait states: covers the MFMA-result -> VALU / memory read hazard and VALU-write -> MFMA srcC
-MIFT_HD void mfma_fence() { asm volatile("s_nop 15\n\ts_nop 15" ::: "memory"); }
-// An empty volatile asm that "rewrites" every accumulator in AGPRs: placed after mfma_fence it keeps
-// ordinary reads / writes of acc on their side of the fence (data dependence on the pinned values).
-template <int TM, int TN>
-MIFT_HD void pin_acc(float4_ (&acc)[TM][TN]) {
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    static_assert(TN == 8, "pin_acc: 8 accumulators per asm");
-    asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
-                 "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
-  }
-}
-
 MIFT_HD float apply_act(int act, float z, float aux) {
   switch (act) {
     case ACT_GELU_TANH: return gelu_tanh(z);
@@ -277,8 +242,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;  // 1-KiB LDS-DMA pieces per stage
   static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "stage pieces must split evenly over waves");
   constexpr int PER_STAGE = (A_INSTR + B_INSTR) / NW;  // vmcnt units per stage per wave
-  // NSTAGE 0 = phased schedule on 2 buffers, 1 = wide-wave schedule on 2 buffers (mainloopW)
-  constexpr int NBUF = NSTAGE <= 1 ? 2 : NSTAGE;
+  constexpr int NBUF = NSTAGE == 0 ? 2 : NSTAGE;       // NSTAGE 0 = phased schedule on 2 buffers
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (ep.sstep != nullptr) {
     ep.seed = mift_seed(ep.seed, ep.sstep);
@@ -492,85 +456,6 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     }
     if (wm == 0) __builtin_amdgcn_s_barrier();  // re-align the rows (equal barrier counts)
    }
-  };
-
-  // ---- wide-wave schedule (NSTAGE == 1): 256x256 tile, 2x2 waves = ONE wave per SIMD owning a
-  // 128x128 quadrant (8x8 MFMA 16x16x32 tiles, 256 accumulator registers), two LDS buffers, ONE
-  // barrier per k-tile.  Per k-tile a wave issues 128 MFMAs (2048 matrix cycles) against 32
-  // ds_read_b128 and 16 LDS-DMA pieces, so the next tile's DMA (issued right after the barrier)
-  // has a whole k-tile of MFMA work to land under.  The phased 8-wave schedule above spent 41 % of
-  // its wave cycles parked at its 8 barriers per k-tile on the K = 768 LM head (SQ_WAIT_ANY,
-  // profiles/r2/pmc_lmhead_vs_hipblaslt.txt), where the library's 4-wave 256x256 kernel parks 12 %.
-  // Hazards: buffer (kt+1)&1 is restaged only after the barrier of k-tile kt, which every wave
-  // passes after its MFMAs of k-tile kt-1 consumed (waited) all its reads of that buffer.
-  auto mainloopW = [&](int kb, int ke, auto&& hook) {
-   if constexpr (NSTAGE == 1) {
-    static_assert(BM == 256 && BN == 256 && NWM == 2 && NWN == 2, "wide-wave loop: 256x256 tile, 2x2 waves");
-    static_assert(STAGE_BYTES == 65536 && A_BYTES == 32768, "stage layout: A rows then B rows, 128 B each");
-    const int nk = ke - kb;
-    const int swz = fr & 7;  // (row & 7) of every fragment row this lane reads
-    const uint32_t lds0 = lds_addr(smem);
-    // per-lane byte offsets of k-step kk's first fragments in a stage; rows i*16 are immediates
-    const uint32_t offA0 = (wm * WM + fr) * ROWB + ((fq ^ swz) << 4);
-    const uint32_t offA1 = (wm * WM + fr) * ROWB + (((4 + fq) ^ swz) << 4);
-    const uint32_t offB0 = A_BYTES + (wn * WN + fr) * ROWB + ((fq ^ swz) << 4);
-    const uint32_t offB1 = A_BYTES + (wn * WN + fr) * ROWB + (((4 + fq) ^ swz) << 4);
-    frag_t<T> fa[2][TM], fb[2][TN];
-    // group g (0..3) of one k-step's 16 fragment reads: B 0-3, B 4-7, A 0-3, A 4-7
-    auto rd4 = [&](frag_t<T>* fb_, frag_t<T>* fa_, uint32_t aA, uint32_t aB, int g) {
-      if (g == 0) { lds_rd<0>(fb_[0], aB); lds_rd<2048>(fb_[1], aB); lds_rd<4096>(fb_[2], aB); lds_rd<6144>(fb_[3], aB); }
-      if (g == 1) { lds_rd<8192>(fb_[4], aB); lds_rd<10240>(fb_[5], aB); lds_rd<12288>(fb_[6], aB); lds_rd<14336>(fb_[7], aB); }
-      if (g == 2) { lds_rd<0>(fa_[0], aA); lds_rd<2048>(fa_[1], aA); lds_rd<4096>(fa_[2], aA); lds_rd<6144>(fa_[3], aA); }
-      if (g == 3) { lds_rd<8192>(fa_[4], aA); lds_rd<10240>(fa_[5], aA); lds_rd<12288>(fa_[6], aA); lds_rd<14336>(fa_[7], aA); }
-    };
-    // prologue: tile 0 landed and visible, tile 1 in flight, k-step 0 fragments of tile 0 read
-    stage(0, kb * BK);
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    stage(1, (kb + min(1, nk - 1)) * BK);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) rd4(fb[0], fa[0], lds0 + offA0, lds0 + offB0, g);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_fence();
-    pin_acc<TM, TN>(acc);  // zero fill / caller's writes -> first MFMA
-    for (int kt = 0; kt < nk; ++kt) {
-      hook(kt);
-      const uint32_t cur = lds0 + (kt & 1) * STAGE_BYTES, nxt = lds0 + ((kt + 1) & 1) * STAGE_BYTES;
-      // k-step 0 of tile kt, k-step 1 fragment reads behind the first four row groups
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) mfma16_acc<T>(acc[i][j], fb[0][j], fa[0][i]);
-        if (i < 4) rd4(fb[1], fa[1], cur + offA1, cur + offB1, i);
-      }
-      // tile kt+1 landed (own pieces), every wave's reads of tile kt done -> restage tile kt's buffer
-      wait_vmcnt<0>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      // unconditional (clamped) restage keeps the body branch-free; extra copies land in a buffer
-      // nobody reads any more and are drained after the loop
-      stage(kt & 1, (kb + min(kt + 2, nk - 1)) * BK);
-      // k-step 1 of tile kt, tile kt+1's k-step 0 reads behind the first four row groups
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) mfma16_acc<T>(acc[i][j], fb[1][j], fa[1][i]);
-        if (i < 4) rd4(fb[0], fa[0], nxt + offA0, nxt + offB0, i);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    wait_vmcnt<0>();  // the clamped extra stages have landed before anything reuses the ring
-    __builtin_amdgcn_s_barrier();
-    mfma_fence();     // last MFMA -> accumulator reads of the epilogue
-    pin_acc<TM, TN>(acc);
-   }
-  };
-  // the 256x256 main loop of this instantiation (phased 8-wave or wide-wave 4-wave)
-  auto bigloop = [&](int kb, int ke, auto&& hook) {
-    if constexpr (NSTAGE == 1) mainloopW(kb, ke, hook);
-    else mainloop8(kb, ke, hook);
   };
 
   // fused epilogue of the (m0, n0) tile from acc (+ LoRA K-extension)
@@ -899,7 +784,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
 
   const int nk_all = K / BK;
   if constexpr (EPI == 1) {
-    static_assert(NSTAGE <= 1, "LM-head forward runs on a 256x256 big-tile loop");
+    static_assert(NSTAGE == 0, "LM-head forward runs on the phased 256x256 tile");
     // one block per tile: a persistent loop over tiles (E stores draining under the next tile's main
     // loop) measured 2-3 % faster in isolation but pushed the kernel past 256 VGPRs into scratch
     // spills; with the row targets in LDS the one-tile kernel needs 220 and no spills
@@ -922,7 +807,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
-      bigloop(0, nk_all, [](int) {});
+      mainloop8(0, nk_all, [](int) {});
       lm_fwd_epilogue();
     }
     return;
@@ -935,7 +820,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     // it at the clamped reference errs by < e^-60 relative), and the chunk's result is
     // acc·exp(ref - lse).  Block -> (tile, split-K chunk of gpc groups); the reduction kernel
     // sums the chunks, subtracts W[label] and applies the upstream gradient.
-    static_assert(NSTAGE <= 1, "LM-head dgrad runs on a 256x256 big-tile loop");
+    static_assert(NSTAGE == 0, "LM-head dgrad runs on the phased 256x256 tile");
     const LmArgs& lm = ep.lm;
     const int S = (lm.ntn + lm.gpc - 1) / lm.gpc;
     const int tl = blockIdx.x / S, cidx = blockIdx.x % S;
@@ -964,14 +849,10 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         if (g < nw) ms[r * cstride + g] = lm.stats[(size_t)min(m0 + r, M - 1) * lm.ntn + w0 + g].x;
       }
       __syncthreads();
-      bigloop(w0 * GK, min(nk_all, w1 * GK), [&](int kt) {
+      mainloop8(w0 * GK, min(nk_all, w1 * GK), [&](int kt) {
         const int gk = w0 * GK + kt;
         if (gk % GK != 0) return;
         const int g = gk / GK - w0;
-        if constexpr (NSTAGE == 1) {  // opaque MFMAs (mfma16_acc) -> VALU reads
-          mfma_fence();
-          pin_acc<TM, TN>(acc);
-        }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const float m = ms[(wm * WM + i * 16 + fr) * cstride + g];
@@ -980,10 +861,6 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
           ref[i] = rn;
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] *= f;
-        }
-        if constexpr (NSTAGE == 1) {  // VALU writes -> MFMA srcC
-          pin_acc<TM, TN>(acc);
-          mfma_fence();
         }
       });
     }
@@ -1015,12 +892,12 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       m0 = tm * BM;
       n0 = tn * BN;
     }
-    if constexpr (NSTAGE <= 1) {
+    if constexpr (NSTAGE == 0) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
-      bigloop(0, nk_all, [](int) {});
+      mainloop8(0, nk_all, [](int) {});
     } else {
       mainloop(0, nk_all);
     }
@@ -1133,7 +1010,7 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
                  int K, const EpiArgs& ep, hipStream_t st) {
   constexpr int STAGE_BYTES = (BM + BN) * ROWB;
   constexpr int EPI_BYTES = BM * CTile<BN>::CLD * 2;
-  constexpr int RING = (NSTAGE <= 1 ? 2 : NSTAGE) * STAGE_BYTES;
+  constexpr int RING = (NSTAGE == 0 ? 2 : NSTAGE) * STAGE_BYTES;
   constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
   constexpr int NT = NWM * NWN * 64;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
@@ -1209,8 +1086,6 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
 //      ragged waves: N=768 gives 512 tiles = exactly one wave of 2x256 slots (128x128: 384)
 //   8: 256x256, 8 waves (2x4), phased schedule (mainloop8: 4 phases per k-tile, staggered wave
 //      rows, counted vmcnt across barriers, setprio MFMA clusters)
-//  10: 256x256, 4 waves (2x2, wave tile 128x128), wide-wave schedule (mainloopW: one barrier per
-//      k-tile, one wave per SIMD)
 //   9: 128x192, 8 waves (2x4, wave tile 64x48), 2-stage ring (80 KiB -> two blocks = 16 waves per
 //      CU): the wide-N distilgpt2 shapes (N = 2304 / 3072, K = 768) ran 20-25 % faster than 128x96 /
 //      128x128 (c_fc fwd 52.6 vs 63.5 us, c_attn fwd 37.2 vs 48.9, c_proj dgrad 62.3 vs 75.7);
@@ -1253,7 +1128,6 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     case 7: launch_gemm<T, 128, 96, 2, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 8: launch_gemm<T, 256, 256, 2, 4, 0>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 9: launch_gemm<T, 128, 192, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
-    case 10: launch_gemm<T, 256, 256, 2, 2, 1>(a, b, c, a2, b2, M, N, K, ep, st); break;
     default: launch_gemm<T, 64, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
   }
 }
@@ -1316,12 +1190,6 @@ __global__ __launch_bounds__(256) void lmhead_reduce_kernel(const float* __restr
   store8<T>(out + (size_t)row * N + c8, acc);
 }
 
-// LM-head kernels: phased 8-wave schedule (default) or the wide-wave 4-wave one (MIFT_LM_WIDE=1)
-bool lm_wide() {
-  const char* e = getenv("MIFT_LM_WIDE");
-  return e ? atoi(e) != 0 : false;
-}
-
 template <typename T>
 std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int V,
                                         int shift) {
@@ -1352,20 +1220,15 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   // staging ring (128 KiB) reused for the E tile + the two row-partial arrays
   constexpr int SMEM = std::max(2 * (BM + BN) * ROWB, BM * CTile<BN>::CLD * 2 + 2 * 8 * (BM / 2) * 4 + BM * 4);
   static_assert(SMEM <= 160 * 1024, "LDS budget");
-  // MIFT_LM_WIDE (read per call, A/B-able): 1 = wide-wave 4-wave kernel, 0 = phased 8-wave (default)
-  const bool wide = lm_wide();
-  auto kern = wide ? gemm_nt_kernel<T, BM, BN, 2, 2, 1, false, 1> : gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>;
+  auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<T, BM, BN, 2, 2, 1, false, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr = true;
   }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const int grid = ntm * ntn;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(wide ? 256 : 512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
                      (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
   hipLaunchKernelGGL(lmhead_lse_kernel, dim3((M + 3) / 4), dim3(256), 0, st,
                      reinterpret_cast<const float2*>(stats.data_ptr<float>()), ntn, zlab.data_ptr<float>(),
@@ -1402,18 +1265,14 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   ep.lm.shift = shift;
   if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   SkArgs sk{};
-  const bool wide = lm_wide();
-  auto kern = wide ? gemm_nt_kernel<T, BM, BN, 2, 2, 1, false, 2> : gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
+  auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<T, BM, BN, 2, 2, 1, false, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr = true;
   }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-  hipLaunchKernelGGL(kern, dim3(tiles * S), dim3(wide ? 256 : 512), SMEM, st, (const T*)E.data_ptr(), (const T*)wt.data_ptr(),
+  hipLaunchKernelGGL(kern, dim3(tiles * S), dim3(512), SMEM, st, (const T*)E.data_ptr(), (const T*)wt.data_ptr(),
                      (T*)nullptr, nullptr, nullptr, M, N, K, (int)E.stride(0), (int)wt.stride(0), N, ep, sk);
   auto out = at::empty({M, N}, E.options());
   const size_t chunks = (size_t)M * (N / 8);
