@@ -142,10 +142,16 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
 
     # prefill over right-aligned prompts: row b = ids[b, start_b:] then padding, positions 0..S0-1
     ar = torch.arange(S0, device=dev)
+    # filler after each right-aligned prompt / input of a finished row: any id INSIDE the embedding
+    # table.  Filler K/V are masked (kv_len, the decode gap) but still multiplied by p = 0 inside the
+    # kernels' P·V, so an out-of-table id (GPT-2's pad = eos = 50256 on a smaller test vocabulary)
+    # read garbage rows and a non-finite V turned 0·V into NaN for the whole row.
+    vocab = model.tied_embedding().shape[0]
+    fill = pad if pad is not None and 0 <= pad < vocab else 0
     if padded:
         src = (ar[None, :] + start[:, None]).clamp(max=S0 - 1)
         ids_r = torch.where(ar[None, :] < lens[:, None], torch.gather(input_ids, 1, src),
-                            torch.full_like(input_ids, pad if pad is not None and pad >= 0 else 0))
+                            torch.full_like(input_ids, fill))
     else:
         ids_r = input_ids
     h = model.embed_at(ids_r, ar[None, :].expand(B, S0).contiguous())
@@ -165,7 +171,7 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
             break
         t = S0 + i
         pos = (lens + i)[:, None]
-        h = model.embed_at(nxt[:, None], pos)
+        h = model.embed_at(torch.where(done, torch.full_like(nxt, fill), nxt)[:, None], pos)
         h = _run_blocks(model, h, lambda li: _decode_attn(cache, li, B, H, hd, t, plen, S0, fused), fused)
         nxt = model.head_logits(h)[:, -1].float().argmax(-1)
     return torch.cat(out, 1)
