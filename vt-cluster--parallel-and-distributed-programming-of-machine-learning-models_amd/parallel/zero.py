@@ -34,10 +34,19 @@ class Zero1AdamW:
         groups = [dp_group] + [g for g in stats_groups if g is not None]
         self.opt = FusedAdamW(arena.param[self.lo:self.hi], self.gshard, reduce_stats_group=groups, **opt_kw)
 
-    # FusedAdamW-compatible surface used by the Trainer
+    # FusedAdamW-compatible surface used by the Trainer (tests/test_zero_surface_cpu.py checks that
+    # every ``self.opt.<name>`` the Trainer touches exists here)
     @property
     def loss_scale_t(self):
         return self.opt.loss_scale_t
+
+    @property
+    def g(self):  # this rank's gradient shard (the Trainer's setup warm-up launches grad_stats on it)
+        return self.opt.g
+
+    @property
+    def stats_buf(self):
+        return self.opt.stats_buf
 
     @property
     def state(self):
