@@ -14,6 +14,6 @@ bash tools/gpu_job.sh \
   "a_p1ckpt:300:python scripts/finetune_lora_distilgpt2.py --dataset medium --synthetic 2048 --max_steps 12 --save_steps 6 --logging_steps 6 --logdir $O/p1_logs --out_root $O/p1_out" \
   "a_tiny:300:python labs/tiny/train_tiny.py --subset 512 --epochs 1 --batch 8 --out $O/tiny_out --no_tb && python labs/tiny/test_tiny.py --ckpt $O/tiny_out && python labs/tiny/infer_ddp.py --ckpt $O/tiny_out --max_test 256" \
   "a_simple:200:python labs/simple_model/train_simple.py --max_steps 4 --output_dir $O/simple" \
-  "a_ft:200:python labs/fine_tuning/fine_tune.py --subset 64 --epochs 1 --output_dir $O/ft" \
-  "a_tl:200:python labs/transfer_learning/transfer.py --epochs 1 --output_dir $O/tl" \
+  "a_ft:200:python labs/fine_tuning/fine_tune.py --max_steps 8 --output_dir $O/ft" \
+  "a_tl:400:python labs/transfer_learning/transfer.py --epochs 1 --output_dir $O/tl" \
   "a_rag:200:python labs/ragging/rag_example.py --subset 200 --max_new_tokens 8"
