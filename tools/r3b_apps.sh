@@ -5,7 +5,7 @@ export MIFT_BACKEND=gloo
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 export TMPDIR=/tmp
-O=gpurun_out/apps
+O=/tmp/apps  # checkpoints stay on the box (the merge back is capped at 64 MiB); logs: gpurun_out/<step>.log
 mkdir -p $O
 TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 bash tools/gpu_job.sh \
