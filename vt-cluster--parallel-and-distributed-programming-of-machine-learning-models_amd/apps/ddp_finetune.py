@@ -195,7 +195,9 @@ def main(argv=None, defaults=None):
             json.dump(meta, f, indent=2)
         print(f"✅ saved adapter + tokenizer to {save_dir}", flush=True)
     logs.log("Model save", time.perf_counter() - t0)
-    tokens = len(batcher.indices(0)) * args.seq_len * ctx.dp * args.epochs
+    # lines actually trained: whole epochs, or global_step full steps when --max_steps stops early
+    lines = min(len(batcher.indices(0)) * args.epochs, trainer.global_step * batcher.mb * batcher.accum)
+    tokens = lines * args.seq_len * ctx.dp
     if rank == 0:
         print(f"[RANK 0] TRAIN_RUNTIME_SEC={train_secs:.3f}", flush=True)
         print(f"[RANK 0] tokens_per_sec={tokens / max(train_secs, 1e-9):.1f} steps={trainer.global_step}", flush=True)
