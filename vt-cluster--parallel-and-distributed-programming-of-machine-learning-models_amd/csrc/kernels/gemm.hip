@@ -1249,6 +1249,7 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   // split the vocabulary so the grid is a whole number of chip waves (one block per CU), >= 3 waves
   const int cus = num_cus();
   int S = std::max(1, std::min(ntn_f, (3 * cus + tiles - 1) / tiles));
+  if (const char* e = getenv("MIFT_LM_SPLIT")) S = std::max(1, std::min(ntn_f, atoi(e)));  // A/B knob, per call
   const int gpc = (ntn_f + S - 1) / S;
   S = (ntn_f + gpc - 1) / gpc;
   auto partial = at::empty({S, M, N}, E.options().dtype(at::kFloat));
