@@ -74,7 +74,7 @@ struct LmArgs {
   int ntn;                // column tiles of the forward (= groups of the backward)
   int gpc;                // groups per split-K chunk
   float* partial;         // [S][M][N] fp32 split-K slabs
-  int dbg;                // MIFT_LM_DBG (diagnostics only): bit 0 = skip the E store
+  int dbg;                // MIFT_LM_DBG (diagnostics only): bit 0 = skip the E store, bit 2 = no FULL-tile epilogue
   int nt;                 // MIFT_LM_NT (A/B): bit 0 = nontemporal E stores (fwd), bit 1 = nt E loads (dgrad)
   int shift;              // > 0: labels are the UNSHIFTED [B*S] ids, S = shift (see lm_label)
 };
@@ -705,54 +705,66 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       const int64_t l = lm_label(lm.labels, min(m0 + tid, M - 1), lm.shift);
       labs[tid] = (l >= 0 && l < V) ? (int)l : -1;
     }
-    const bool full = n0 + BN <= V;  // block-uniform: only the last column tile holds padding columns
+    // Two instantiations of the exp epilogue: every column tile but the last is FULL (no padding
+    // columns), and there it needs no per-element bounds selects; the label's logit is picked by
+    // selects across the row's column tiles and stored once per row fragment (one divergent store
+    // per i instead of one exec-mask branch per (i, j)).
+    const bool dbg_raw = (lm.dbg & 2) != 0;
+    auto exp_pass = [&](auto fullc) {
+      constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      float m = -INFINITY;
+      for (int i = 0; i < TM; ++i) {
+        float m = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * WN + j * 16 + fq * 4;
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * WN + j * 16 + fq * 4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m = (full || col + e < V) ? fmaxf(m, acc[i][j][e]) : m;
-      }
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      if (fq == 0) redm[wave * WM + i * 16 + fr] = m;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      float m = -INFINITY;
-#pragma unroll
-      for (int w = 0; w < NWN; ++w) m = fmaxf(m, redm[(wm * NWN + w) * WM + i * 16 + fr]);
-      if (m == -INFINITY) m = 0.f;  // tile entirely beyond V (cannot happen for V_pad - V < BN)
-      const int lrow = wm * WM + i * 16 + fr;
-      const int row = m0 + lrow;
-      const int lab = row < M ? labs[lrow] : -1;
-      const float mb = m * L2E;
-      float s = 0.f;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int lcol = wn * WN + j * 16 + fq * 4;
-        const int col = n0 + lcol;
-        float ev[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ev[e] = (lm.dbg & 2) ? acc[i][j][e]
-                  : (full || col + e < V) ? __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][e], L2E, -mb)) : 0.f;
-          s += ev[e];
+          for (int e = 0; e < 4; ++e) m = (FULL || col + e < V) ? fmaxf(m, acc[i][j][e]) : m;
         }
-        const int d = lab - col;
-        if (d >= 0 && d < 4) {  // static selects: a runtime vector index would go to scratch
-          const float4_ a = acc[i][j];
-          lm.zlab[row] = d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
-        }
-        store4<T>(Cs + CT::off4(lrow, lcol), ev);
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        if (fq == 0) redm[wave * WM + i * 16 + fr] = m;
       }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (fq == 0) reds[wave * WM + i * 16 + fr] = s;
-    }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < NWN; ++w) m = fmaxf(m, redm[(wm * NWN + w) * WM + i * 16 + fr]);
+        if (m == -INFINITY) m = 0.f;  // tile entirely beyond V (cannot happen for V_pad - V < BN)
+        const int lrow = wm * WM + i * 16 + fr;
+        const int row = m0 + lrow;
+        const int lab = row < M ? labs[lrow] : -1;
+        const float mb = m * L2E;
+        float s = 0.f, zl = 0.f;
+        bool hit = false;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int lcol = wn * WN + j * 16 + fq * 4;
+          const int col = n0 + lcol;
+          float ev[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ev[e] = dbg_raw ? acc[i][j][e]
+                    : (FULL || col + e < V) ? __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][e], L2E, -mb)) : 0.f;
+            s += ev[e];
+          }
+          const int d = lab - col;  // static selects: a runtime vector index would go to scratch
+          const float4_ a4 = acc[i][j];
+          const float v = d == 0 ? a4[0] : d == 1 ? a4[1] : d == 2 ? a4[2] : a4[3];
+          const bool h = d >= 0 && d < 4;
+          zl = h ? v : zl;
+          hit = hit || h;
+          store4<T>(Cs + CT::off4(lrow, lcol), ev);
+        }
+        if (hit) lm.zlab[row] = zl;
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (fq == 0) reds[wave * WM + i * 16 + fr] = s;
+      }
+    };
+    if (n0 + BN <= V && !(lm.dbg & 4)) exp_pass(std::true_type{});  // block-uniform; dbg bit 2: A/B
+    else exp_pass(std::false_type{});
     __syncthreads();
     if (tid < BM) {  // one thread per block row: combine the NWN wave partials
       const int wr = tid / WM, rr = tid % WM;
