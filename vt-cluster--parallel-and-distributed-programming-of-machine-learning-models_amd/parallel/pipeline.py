@@ -50,6 +50,7 @@ loss by ``loss_scale / global_ntokens`` (token-count normalisation over the
 whole optimizer step and all DP replicas), so PP, DP and single-GPU runs
 produce the same update for the same data.
 """
+import gc
 import os
 from collections import deque
 
@@ -412,14 +413,21 @@ class _StageGraphs:
                     invalidate_packs(e.model)
                 C().set_seed_step(sl["step"])
                 gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gf, capture_error_mode="thread_local"):
-                    y = e._forward(sl["inp"], sl.get("x"), 0)
-                with torch.cuda.graph(gb, pool=gf.pool(), capture_error_mode="thread_local"):
-                    if e.last:
-                        (y * self.gs).backward(retain_graph=True)
-                    else:
-                        torch.autograd.backward(y, grad_tensors=sl["g"], retain_graph=True)
-                    streams.join()
+                gc_was = gc.isenabled()
+                gc.collect()
+                gc.disable()  # no collection inside the captures (see train/graph.py)
+                try:
+                    with torch.cuda.graph(gf, capture_error_mode="thread_local"):
+                        y = e._forward(sl["inp"], sl.get("x"), 0)
+                    with torch.cuda.graph(gb, pool=gf.pool(), capture_error_mode="thread_local"):
+                        if e.last:
+                            (y * self.gs).backward(retain_graph=True)
+                        else:
+                            torch.autograd.backward(y, grad_tensors=sl["g"], retain_graph=True)
+                        streams.join()
+                finally:
+                    if gc_was:
+                        gc.enable()
                 C().set_seed_step(None)
                 sl.update(gf=gf, gb=gb, y=y, gx=(sl["x"].grad if not e.first else None))
                 self.slots.append(sl)

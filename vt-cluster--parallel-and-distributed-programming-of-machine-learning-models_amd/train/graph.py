@@ -28,6 +28,7 @@ Captures are keyed by the micro-batch shapes (the last, shorter step of an
 epoch gets its own graph or runs eagerly); the first step of every shape runs
 eagerly as warm-up (lazy library init, workspace allocation).
 """
+import gc
 import os
 
 import torch
@@ -130,12 +131,19 @@ class GraphedStep:
         graph_seeds(True)
         streams.set_enabled(os.environ.get("MIFT_GRAPH_SIDE", "0") == "1")
         red = tr.reducer
+        # no Python GC inside the capture: torch.cuda.graph collects once at entry, but a collection
+        # triggered mid-capture ran finalizers of device objects and aborted the process (seen once
+        # in tests/test_graph_gpu.py, GC-timing dependent)
+        gc_was = gc.isenabled()
+        gc.disable()
         try:
             # collectives are never captured: the DP buckets launch after the replay (finish())
             with (red.no_sync() if red is not None else _nullctx()):
                 with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
                     self._fwd_bwd(ent, len(mbs))
         finally:
+            if gc_was:
+                gc.enable()
             graph_seeds(False)
             streams.set_enabled(None)
             _C().set_seed_step(None)
