@@ -10,8 +10,21 @@ OpenWebText-shaped tokens, random-init weights (no network).  One "step" =
 one full optimizer step (forward, backward, gradient all-reduce over RCCL,
 fused AdamW).  Weak scaling: every rank processes 32 x 256 tokens per step.
 
-  python bench.py --gpus N --steps K --warmup W
-  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+  python bench.py --gpus N --steps K --warmup W [--config {1..5}]
+
+With N > 1 and no torchrun environment (WORLD_SIZE unset) this process starts the N ranks itself:
+it runs ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1`` on this file
+as a CHILD process (the parent never touches the GPU and never execs) and exits with its code.
+Under torchrun (``WORLD_SIZE`` set, as the driver launches it) the formed world must equal
+``--gpus``, else the run exits non-zero instead of silently measuring a different world.
+``MIFT_BACKEND=gloo`` keeps the same command usable as an N-rank rehearsal on one GPU.
+
+``--config`` selects a BASELINE.json config (recorded as ``config.config_id``):
+  1  distilgpt2 LoRA DDP, world 1, CPU / gloo, fp32 (plumbing)
+  2  distilgpt2 LoRA DDP bf16, 1..8 GPUs (default; the headline)
+  3  OPT-2.7B fp16 LoRA, 4-stage pipeline (--gpus 4)
+  4  OPT-2.7B fp16 LoRA, 2 DP x 4 PP (--gpus 8)
+  5  OPT-6.7B fp16 LoRA, 8-stage pipeline (--gpus 8)
 
 Prints ONE JSON line on rank 0.  `value` = whole-job steady-state tokens/s over the K timed
 steps; ``wall_clock_epoch_s`` = one full epoch over a 20k-line medium_openwebtext-shaped
@@ -29,29 +42,109 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
-def main():
+# BASELINE.json "configs" -> bench presets (the reference's P1 / P2 shapes)
+CONFIGS = {
+    1: dict(model="distilgpt2", gpus=1, pp=1, precision="fp32", device="cpu", impl="torch",
+            steps=2, warmup=1, epoch_lines=0),
+    2: dict(model="distilgpt2", gpus=1, pp=1, precision="bf16"),
+    3: dict(model="facebook/opt-2.7b", gpus=4, pp=4, precision="fp16"),
+    4: dict(model="facebook/opt-2.7b", gpus=8, pp=4, precision="fp16"),
+    5: dict(model="facebook/opt-6.7b", gpus=8, pp=8, precision="fp16"),
+}
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--model", default="distilgpt2")
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default: the config's")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS), help="BASELINE.json config id")
+    ap.add_argument("--steps", type=int, default=None, help="timed optimizer steps (default 50)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warmup steps (default 10)")
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--device", default=None, choices=["gpu", "cpu"],
+                    help="cpu: the world_size>=1 gloo/CPU plumbing path (config 1); default gpu")
     ap.add_argument("--seq_len", type=int, default=None, help="default 256 (GPT-2) / 512 (OPT, P2 sbatch)")
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--accum", type=int, default=None, help="default 32 (P1) / 96 (P2 sbatch)")
     ap.add_argument("--fold_accum", type=int, default=1)
-    ap.add_argument("--micro_batch", type=int, default=0, help="regroup batch*accum into micro-batches of this size")
-    ap.add_argument("--pp", type=int, default=1, help="pipeline stages (world = dp x pp)")
+    ap.add_argument("--micro_batch", default="0",
+                    help="regroup batch*accum into micro-batches of this size; 'auto' (PP default): "
+                         "mift.parallel.plan's HBM-bounded cost model")
+    ap.add_argument("--pp", type=int, default=None, help="pipeline stages (world = dp x pp)")
     ap.add_argument("--partition", default="balanced", choices=["uniform", "balanced"])
     ap.add_argument("--zero", type=int, default=0)
-    ap.add_argument("--precision", default=None, choices=["bf16", "fp16"], help="default bf16 (GPT-2) / fp16 (OPT)")
-    ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
+    ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "fp32"],
+                    help="default bf16 (GPT-2) / fp16 (OPT)")
+    ap.add_argument("--impl", default=None, choices=["fused", "torch"],
                     help="fused = mift HIP kernels; torch = eager PyTorch ops on the same model (comparison)")
     ap.add_argument("--profile_dir", default=None, help="torch.profiler chrome trace of 3 steps")
     ap.add_argument("--epoch_lines", type=int, default=None,
                     help="after the timed steps, run one full epoch over this many medium_openwebtext-shaped "
                          "lines (README.md:66: ~20k) sharded over the DP ranks and report its wall clock "
                          "(the reference's [Training] sec metric); default 20000 for GPT-2, 0 (skip) for OPT")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
+    c = CONFIGS[a.config]
+    a.model = a.model or c["model"]
+    a.gpus = a.gpus if a.gpus is not None else c["gpus"]
+    a.pp = a.pp if a.pp is not None else c["pp"]
+    a.precision = a.precision or c["precision"]
+    a.device = a.device or c.get("device", "gpu")
+    a.impl = a.impl or c.get("impl", "torch" if a.device == "cpu" else "fused")
+    a.steps = a.steps if a.steps is not None else c.get("steps", 50)
+    a.warmup = a.warmup if a.warmup is not None else c.get("warmup", 10)
+    if a.epoch_lines is None:
+        a.epoch_lines = c.get("epoch_lines", 0 if "opt" in a.model.lower() else 20000)
+    if a.micro_batch == "0" and a.pp > 1:
+        a.micro_batch = "auto"
+    return a
+
+
+def fail(msg, code=2):
+    print(f"bench.py: error: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(a):
+    """Start the N ranks as a child ``torch.distributed.run`` (this process stays GPU-free: no HIP
+    call, no exec) and return its exit code.  The worker ranks re-parse the same argv."""
+    import subprocess
+    if a.device != "cpu" and os.environ.get("MIFT_BACKEND", "nccl") != "gloo":
+        import torch  # device_count() does not initialise HIP on this image
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            fail(f"--gpus {a.gpus} needs {a.gpus} visible GPUs for one rank per GPU over RCCL, found {have} "
+                 f"(MIFT_BACKEND=gloo rehearses N ranks on fewer GPUs; --device cpu runs the CPU path)")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 8) // (2 * a.gpus))))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench.py: launching {a.gpus} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
+def main():
+    a = parse_args()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch(a))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != a.gpus:
+        fail(f"--gpus {a.gpus} but the launcher formed WORLD_SIZE={world_env}")
+    if a.gpus % a.pp:
+        fail(f"--gpus {a.gpus} is not a multiple of the {a.pp} pipeline stages of config {a.config}")
+    if a.device == "cpu":
+        os.environ["MIFT_DEVICE"] = "cpu"
+    elif os.environ.get("MIFT_BACKEND", "nccl") != "gloo":
+        import torch
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        if torch.cuda.device_count() < lw:
+            fail(f"{lw} local ranks need {lw} GPUs for RCCL, found {torch.cuda.device_count()}")
     # RCCL / Gloo print their init banners on fd 1 from native code; route
     # everything but the result line to stderr so stdout is exactly ONE JSON line.
     sys.stdout.flush()
@@ -73,26 +166,31 @@ def main():
     is_opt = "opt" in a.model.lower()
     a.seq_len = a.seq_len or (512 if is_opt else 256)
     a.accum = a.accum or (96 if is_opt else 32)
-    a.precision = a.precision or ("fp16" if is_opt else "bf16")
-    if a.epoch_lines is None:
-        a.epoch_lines = 0 if is_opt else 20000
     ctx = D.init(pp=a.pp, verbose=False, sanity=True)
-    if a.gpus != ctx.world:
-        if ctx.rank == 0:
-            print(f"warning: --gpus {a.gpus} != WORLD_SIZE {ctx.world}; using WORLD_SIZE", file=sys.stderr)
     n = ctx.world
-    assert ctx.device.type == "cuda", "bench.py needs a GPU"
+    if n != a.gpus or ctx.pp != a.pp:
+        fail(f"formed world {n} (pp {ctx.pp}) differs from --gpus {a.gpus} --pp {a.pp}")
+    on_gpu = ctx.device.type == "cuda"
+    if a.device == "gpu" and not on_gpu:
+        fail("no GPU visible (use --device cpu / --config 1 for the CPU plumbing path)")
     if a.impl == "fused":
-        assert mift.kernels_available(), f"HIP extension not loaded: {mift._ext.error()!r}"
-    dtype = torch.bfloat16 if a.precision == "bf16" else torch.float16
+        if not on_gpu:
+            fail("--impl fused needs a GPU")
+        if not mift.kernels_available():
+            fail(f"HIP extension not loaded: {mift._ext.error()!r}")
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.precision]
+
+    def sync():
+        if on_gpu:
+            sync()
 
     split = None
     kw = {}
+    from mift.models.opt import OPTConfig
+    from mift.models.gpt2 import GPT2Config
+    mcfg = OPTConfig.preset(a.model) if is_opt else GPT2Config.preset(a.model)
     if ctx.pp > 1:
-        from mift.models.opt import OPTConfig
-        from mift.models.gpt2 import GPT2Config
         from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
-        mcfg = OPTConfig.preset(a.model) if is_opt else GPT2Config.preset(a.model)
         split = partition_layers(mcfg.num_layers(), ctx.pp, a.partition, head_cost_layers(mcfg))
         kw = dict(layer_range=stage_layer_range(split, ctx.pp_rank), has_embed=ctx.is_first_stage,
                   has_head=ctx.is_last_stage)
@@ -103,8 +201,13 @@ def main():
     if a.impl == "torch":
         model.fused = False
     per_rank = a.batch * a.accum
-    if a.micro_batch and per_rank % a.micro_batch == 0:
-        mb, acc = a.micro_batch, per_rank // a.micro_batch
+    plan = None
+    if a.micro_batch == "auto" and ctx.pp > 1:
+        from mift.parallel.plan import choose_micro_batch
+        plan = choose_micro_batch(mcfg, a.seq_len, per_rank, ctx.pp, dtype_bytes=dtype.itemsize, name=a.model)
+        mb, acc = plan["micro_batch"], per_rank // plan["micro_batch"]
+    elif a.micro_batch not in ("0", "auto") and per_rank % int(a.micro_batch) == 0:
+        mb, acc = int(a.micro_batch), per_rank // int(a.micro_batch)
     else:
         mb, acc = (per_rank, 1) if (a.fold_accum and ctx.pp == 1) else (a.batch, a.accum)
     total_steps = a.warmup + a.steps
@@ -123,25 +226,26 @@ def main():
 
     for i in range(a.warmup):
         run(i)
-    torch.cuda.synchronize()
+    sync()
     if dist.is_initialized():
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     trace = os.environ.get("MIFT_BENCH_TRACE") == "1"  # diagnostics: per-step host ms to stderr
     sync_every = int(os.environ.get("MIFT_BENCH_SYNC", "0"))  # diagnostics: host sync every k steps
     t0 = time.perf_counter()
     for i in range(a.warmup, total_steps):
         run(i)
         if trace or (sync_every and (i + 1) % sync_every == 0):
-            torch.cuda.synchronize()
+            sync()
         if trace:
             print(f"step {i} {(time.perf_counter() - t0) * 1000:.2f}", file=sys.stderr)
-    torch.cuda.synchronize()
+    sync()
     if dist.is_initialized():
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
+    red_dev = ctx.device if ctx.backend == "nccl" else "cpu"
+    t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
     if dist.is_initialized() and n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = t.item()
@@ -154,7 +258,7 @@ def main():
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
             for i in range(min(3, len(steps))):
                 run(i % len(steps))
-            torch.cuda.synchronize()
+            sync()
         os.makedirs(a.profile_dir, exist_ok=True)
         prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
         with open(os.path.join(a.profile_dir, "table.txt"), "w") as f:
@@ -169,16 +273,16 @@ def main():
 
         def timed_epoch(trainer):
             eb_steps = list(MicroBatcher(eds, mb, acc, rank=ctx.dp_rank, world=ctx.dp).epoch(0))
-            torch.cuda.synchronize()
+            sync()
             if dist.is_initialized():
                 dist.barrier()
             te = time.perf_counter()
             for s_ in eb_steps:
                 trainer.train_step(s_)
-            torch.cuda.synchronize()
+            sync()
             if dist.is_initialized():
                 dist.barrier()
-            tt = torch.tensor([time.perf_counter() - te], dtype=torch.float64, device=ctx.device)
+            tt = torch.tensor([time.perf_counter() - te], dtype=torch.float64, device=red_dev)
             if dist.is_initialized() and n > 1:
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             return round(tt.item(), 4), len(eb_steps)
@@ -194,13 +298,13 @@ def main():
         model2 = build_causal_lm(a.model, dtype=dtype, device=ctx.device, seed=0, **kw)
         L.inject(model2, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=targets,
                                       base_model_name_or_path=a.model))
-        torch.cuda.synchronize()
+        sync()
         ts = time.perf_counter()
         tr2 = Trainer(model2, MicroBatcher(eds, mb, acc, rank=ctx.dp_rank, world=ctx.dp),
                       TrainConfig(epochs=1, batch=mb, accum=acc, lr=5e-5, precision=a.precision, logging_steps=0,
                                   save_steps=0, step_log="none", zero_stage=a.zero), ctx)
         model2.train()
-        torch.cuda.synchronize()
+        sync()
         setup_s = round(time.perf_counter() - ts, 4)
         epoch_s, epoch_steps = timed_epoch(tr2)
     par = f"dp{ctx.dp}" + (f"xpp{ctx.pp}" if ctx.pp > 1 else "") + ("+zero1" if a.zero and ctx.dp > 1 else "")
@@ -220,10 +324,11 @@ def main():
             "vs_baseline": None,
             "dtype": a.precision,
             "data": f"synthetic (OpenWebText-shaped random tokens, full {a.seq_len}-token lines); random-init weights",
-            "config": {"model": a.model, "global_batch": per_rank * ctx.dp, "seq_len": a.seq_len,
+            "config": {"model": a.model, "config_id": a.config, "global_batch": per_rank * ctx.dp,
+                       "seq_len": a.seq_len, "backend": ctx.backend, "device": ctx.device.type,
                        "parallelism": par, "per_rank_batch": f"{a.batch}x{a.accum}", "micro_batch": f"{mb}x{acc}",
                        "split": split, "lora": "r8/a16/p0.05 " + ",".join(targets), "impl": a.impl,
-                       "tokens_per_gpu_per_s": round(value / n, 1),
+                       "tokens_per_gpu_per_s": round(value / n, 1), "micro_batch_plan": plan,
                        "final_grad_norm": round(stats["grad_norm"], 4)},
             "wall_clock_epoch_s": epoch_s,
             "epoch": {"lines": a.epoch_lines, "steps": epoch_steps, "global_batch": per_rank * ctx.dp,

@@ -1,0 +1,133 @@
+"""Pipeline micro-batch planner: pick the micro-batch size of a PP run for 288 GB HBM.
+
+The reference runs DeepSpeed's 1F1B with micro-batch 1 and 96 micro-batches per optimizer step
+(`P2/submit_opt27b_pp.sbatch:26-32`); on MI355X that shape leaves the matrix cores
+idle (a 512-row GEMM), while one huge micro-batch maximises the pipeline bubble.  For a fixed
+per-replica batch B (sequences per optimizer step), S stages and micro-batch mb (m = B / mb
+micro-batches):
+
+    step(mb) ≈ (m + S − 1) · T_stage(mb) + 2 (S − 1) · hop(mb)
+    T_stage(mb) = max over stages of  layers_s · c_layer(mb·seq) · mb·seq  (+ embed / head work)
+    hop(mb)     = mb·seq·d·bytes / link_bw + link_latency
+
+``c_layer(T)`` is the measured per-token cost of one decoder layer's forward + backward at a
+micro-batch of T tokens on one GPU (``tools/mb_sweep.py``, dp1, graph-replayed steps), kept per
+model in ``MEASURED``; between samples it is interpolated in log(T), outside them the
+``c_inf · (1 + T0 / T)`` fit is used.  The memory bound: stage s keeps up to S − s micro-batches
+of saved activations alive (1F1B), so stage 0 needs S · mb · seq · act_bytes_per_token · layers_0
+on top of its weights; candidates that do not fit ``hbm_budget`` are dropped.
+
+``choose_micro_batch`` returns the fastest feasible mb together with the prediction, including
+the per-GPU efficiency against the best dp1 micro-batch (one GPU, no bubble), so a run records
+WHY it used the micro-batch it used.
+"""
+import math
+
+GiB = 1 << 30
+
+# ms per sequence of a whole dp1 optimizer step (all layers + embed + head + optimizer), seq 512,
+# 96 sequences per step, fp16, fused HIP path, graph replay: tools/mb_sweep.py on one MI355X.
+# Source: profiles/r4/mb_sweep_*.jsonl (filled from the GPU sweep; the r3 pair for OPT-2.7B is
+# mb 4 -> 1132 ms / 96 and mb 48 -> 642 ms / 96, profiles/r3/rehearse_opt27b_pp4.json).
+MEASURED = {
+    "opt-2.7b": {4: 11.79, 48: 6.69},
+}
+
+LINK_BW = 100e9        # bytes/s one xGMI link achieves for a large RCCL p2p (≈153 GB/s raw)
+LINK_LAT = 20e-6       # s per p2p message
+
+
+def _norm(name):
+    return name.lower().split("/")[-1]
+
+
+def cost_per_seq_ms(model_name, mb, measured=None):
+    """dp1 ms per sequence at micro-batch ``mb`` (interpolated in log(mb) between samples)."""
+    tab = (measured or MEASURED).get(_norm(model_name))
+    if not tab:
+        tab = MEASURED["opt-2.7b"]
+    xs = sorted(tab)
+    if mb in tab:
+        return tab[mb]
+    if len(xs) >= 2 and xs[0] <= mb <= xs[-1]:
+        for lo, hi in zip(xs, xs[1:]):
+            if lo <= mb <= hi:
+                f = (math.log(mb) - math.log(lo)) / (math.log(hi) - math.log(lo))
+                return tab[lo] + f * (tab[hi] - tab[lo])
+    # c(mb) = c_inf (1 + m0 / mb) through the two extreme samples
+    a, b = xs[0], xs[-1]
+    ca, cb = tab[a], tab[b]
+    if a == b or ca <= cb:
+        return tab[min(xs, key=lambda x: abs(x - mb))]
+    den = cb / a - ca / b
+    m0 = (ca - cb) / den if den > 0 else 0.0
+    m0 = max(m0, 0.0)
+    c_inf = cb / (1.0 + m0 / b)
+    return c_inf * (1.0 + m0 / mb)
+
+
+def _divisors(n):
+    return [d for d in range(1, n + 1) if n % d == 0]
+
+
+def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_bytes=2, name=None):
+    """Predicted step time and per-GPU efficiency of an S-stage pipeline at micro-batch ``mb``."""
+    name = name or getattr(cfg, "name_or_path", None) or "opt-2.7b"
+    L = cfg.num_layers() if hasattr(cfg, "num_layers") else cfg.num_hidden_layers
+    d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd")
+    m = per_replica // mb
+    seq_ms = cost_per_seq_ms(name, mb, measured)          # whole model, dp1, per sequence
+    # stage share: the balanced partition equalises layers + head (the head ≈ V/(12 d) layers)
+    head_layers = cfg.vocab_size / (12.0 * d)
+    if split is None:
+        t_stage_frac = (L + head_layers) / stages / (L + head_layers)
+    else:
+        costs = [n + (head_layers if i == len(split) - 1 else 0.0) for i, n in enumerate(split)]
+        t_stage_frac = max(costs) / (L + head_layers)
+    t_stage = seq_ms * 1e-3 * mb * t_stage_frac
+    hop = mb * seq * d * dtype_bytes / LINK_BW + LINK_LAT
+    step = (m + stages - 1) * t_stage + 2 * (stages - 1) * hop
+    best_dp1 = min(cost_per_seq_ms(name, x, measured) for x in _divisors(per_replica))
+    dp1_step_per_gpu = best_dp1 * 1e-3 * per_replica / stages   # same work on S GPUs without a bubble
+    return {"micro_batch": mb, "micro_batches": m, "stage_ms": round(t_stage * 1e3, 3),
+            "hop_ms": round(hop * 1e3, 4), "step_ms": round(step * 1e3, 2),
+            "bubble": round((stages - 1) / (m + stages - 1), 4),
+            "efficiency_vs_dp1": round(dp1_step_per_gpu / step, 4)}
+
+
+def act_bytes_per_token_layer(cfg, dtype_bytes=2):
+    """Saved activations of one decoder layer per token (fused path, no recompute): LN outputs,
+    q/k/v/attention output, the FFN pre-activation and post-activation, residuals, LoRA T
+    operands — about 16·d + 2·ffn elements."""
+    d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd")
+    ffn = getattr(cfg, "ffn_dim", None) or 4 * d
+    return (16 * d + 2 * ffn) * dtype_bytes
+
+
+def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=288 * 10 ** 9,
+                       hbm_frac=0.85, measured=None, name=None, candidates=None):
+    """The feasible micro-batch (divisor of ``per_replica``) with the shortest predicted step."""
+    L = cfg.num_layers() if hasattr(cfg, "num_layers") else cfg.num_hidden_layers
+    n_params = getattr(cfg, "num_params", None)
+    d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd")
+    ffn = getattr(cfg, "ffn_dim", None) or 4 * d
+    layer_params = 4 * d * d + 2 * d * ffn
+    weights = (layer_params * L / stages + cfg.vocab_size * d) * dtype_bytes
+    budget = hbm_bytes * hbm_frac - weights
+    per_tok = act_bytes_per_token_layer(cfg, dtype_bytes) * math.ceil(L / stages)
+    best, table = None, []
+    for mb in candidates or _divisors(per_replica):
+        need = stages * mb * seq * per_tok          # stage 0 holds S micro-batches in flight
+        p = predict(cfg, seq, per_replica, stages, mb, measured=measured, dtype_bytes=dtype_bytes, name=name)
+        p["act_gib"] = round(need / GiB, 2)
+        p["fits"] = need <= budget
+        table.append(p)
+        if p["fits"] and (best is None or p["step_ms"] < best["step_ms"]):
+            best = p
+    if best is None:
+        best = table[0]
+    out = dict(best)
+    out["candidates"] = [{k: t[k] for k in ("micro_batch", "step_ms", "efficiency_vs_dp1", "fits")} for t in table]
+    out["model"] = "step = (m+S-1)*T_stage(mb) + 2(S-1)*hop; T_stage from the dp1 mb sweep"
+    del n_params
+    return out
