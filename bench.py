@@ -131,13 +131,13 @@ def launch(a):
 
 def main():
     a = parse_args()
+    if a.gpus < 1 or a.gpus % a.pp:
+        fail(f"--gpus {a.gpus} is not a multiple of the {a.pp} pipeline stages of config {a.config}")
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.exit(launch(a))
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != a.gpus:
         fail(f"--gpus {a.gpus} but the launcher formed WORLD_SIZE={world_env}")
-    if a.gpus % a.pp:
-        fail(f"--gpus {a.gpus} is not a multiple of the {a.pp} pipeline stages of config {a.config}")
     if a.device == "cpu":
         os.environ["MIFT_DEVICE"] = "cpu"
     elif os.environ.get("MIFT_BACKEND", "nccl") != "gloo":

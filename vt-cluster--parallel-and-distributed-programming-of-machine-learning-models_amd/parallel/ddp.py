@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 
 from ..obs.profiler import rng
+from ..utils.faults import maybe_inject
 
 
 class GradReducer:
@@ -63,6 +64,7 @@ class GradReducer:
                 self._p2b[id(p)] = i
         self._off2p = {off: p for (_, p), off in named}
         self._fused = set()  # ids of tensors whose grads the fused backward reports (hooks ignored)
+        self.step = 0        # optimizer step being reduced (set by begin_step; fault injection only)
         self._hooks = []
         self.launch_log = []  # (bucket index, "backward" | "finish") per launch of the last step
         if self.overlap:
@@ -85,6 +87,7 @@ class GradReducer:
             from ..ops.streams import join
             join()  # wgrad kernels queued on the side stream are ordered before the collective
         sl = self.arena.grad[b["lo"]:b["hi"]]
+        maybe_inject(dist.get_rank(), self.step, "grads", grads=sl)
         with rng(f"mift.comm.bucket{b['idx']}.{where}"):
             self.handles.append(dist.all_reduce(sl, group=self.group, async_op=True))
         b["launched"] = True
@@ -131,8 +134,14 @@ class GradReducer:
             b["pending"] = len(b["params"])
             b["launched"] = False
 
-    def begin_step(self):
+    def begin_step(self, step=None):
+        """Start an optimizer step.  Claims are per step: the fused forward re-claims its tensors in
+        every micro-step it runs, so a tensor whose backward this step takes a non-fused path (a shape
+        or flag the fused Functions do not handle) counts through its hook again."""
         self.launch_log = []
+        self._fused.clear()
+        if step is not None:
+            self.step = step
 
     def remove(self):
         for h in self._hooks:

@@ -124,7 +124,7 @@ class PipelineEngine:
         self.prev = ctx.pp_ranks[self.s - 1] if not self.first else None
         self.next = ctx.pp_ranks[self.s + 1] if not self.last else None
         self.mode = os.environ.get("MIFT_PP_P2P", "link")
-        if self.mode == "link":
+        if self.mode in ("link", "blocking"):
             lf, lb = getattr(ctx, "link_f", [None, None]), getattr(ctx, "link_b", [None, None])
             self.rx_f, self.tx_f = P2P(lf[0]), P2P(lf[1])   # activations: from prev / to next
             self.rx_b, self.tx_b = P2P(lb[1]), P2P(lb[0])   # gradients: from next / to prev
@@ -132,9 +132,6 @@ class PipelineEngine:
             f, b = P2P(getattr(ctx, "pp_fwd_group", None)), P2P(getattr(ctx, "pp_bwd_group", None))
             self.rx_f = self.tx_f = f
             self.rx_b = self.tx_b = b
-        elif self.mode == "blocking":
-            g = P2P(getattr(ctx, "pp_group", None))
-            self.rx_f = self.tx_f = self.rx_b = self.tx_b = g
         else:
             raise ValueError(f"MIFT_PP_P2P={self.mode!r}: link | shared | blocking")
         self.blocking = self.mode == "blocking"
@@ -364,11 +361,14 @@ class _StageGraphs:
     overwrote slot k+1's saved activations (measured: NaN gradients from the first replayed step).
     Within a slot the order is the capture order (forward, then backward)."""
 
-    def __init__(self, eng):
+    def __init__(self, eng, max_sets=None):
+        from collections import OrderedDict
         self.e = eng
-        self.sig = None
         self.seen = set()
-        self.slots = None
+        # captured slot sets per micro-batch signature (LRU, bounded): an epoch whose last step has
+        # a different shape replays its own set instead of evicting and recapturing the main one
+        self.sets = OrderedDict()
+        self.max_sets = max_sets or int(os.environ.get("MIFT_PP_GRAPH_SETS", "2"))
         self.gs = torch.zeros((), dtype=torch.float32, device=eng.device)
 
     @staticmethod
@@ -379,13 +379,17 @@ class _StageGraphs:
         if any(self._signature([mb]) != self._signature([mbs[0]]) for mb in mbs):
             return None
         sig = self._signature(mbs)
-        if self.slots is None or self.sig != sig:
+        slots = self.sets.get(sig)
+        if slots is None:
             if sig not in self.seen:
                 self.seen.add(sig)
                 return None  # eager warm-up step for this shape; capture on the next one
-            self._capture(mbs)
-            self.sig = sig
-        return _GraphRun(self, mbs, gscale, micro_step0)
+            while len(self.sets) >= self.max_sets:
+                self.sets.popitem(last=False)  # least recently used signature
+            slots = self._capture(mbs)
+            self.sets[sig] = slots
+        self.sets.move_to_end(sig)
+        return _GraphRun(self, slots, mbs, gscale, micro_step0)
 
     def _capture(self, mbs):
         from ..models.layers import graph_seeds
@@ -394,7 +398,7 @@ class _StageGraphs:
         from ..ops.fused import invalidate_packs
         e = self.e
         K = e.K
-        self.slots = []
+        slots = []
         torch.cuda.synchronize(e.device)
         graph_seeds(True)
         streams.set_enabled(False)
@@ -430,20 +434,23 @@ class _StageGraphs:
                         gc.enable()
                 C().set_seed_step(None)
                 sl.update(gf=gf, gb=gb, y=y, gx=(sl["x"].grad if not e.first else None))
-                self.slots.append(sl)
+                slots.append(sl)
         finally:
             graph_seeds(False)
             streams.set_enabled(None)
             C().set_seed_step(None)
         e.stats["fwd"] -= K  # the captures ran _forward once per slot (backward bypassed _backward)
+        e.stats["captures"] = e.stats.get("captures", 0) + 1
         torch.cuda.synchronize(e.device)
+        return slots
 
 
 class _GraphRun:
     """Replay-based per-micro-batch compute of one ``train_batch`` (slot = i mod K)."""
 
-    def __init__(self, gr, mbs, gscale, micro_step0):
+    def __init__(self, gr, slots, mbs, gscale, micro_step0):
         self.gr, self.e, self.mbs, self.ms0 = gr, gr.e, mbs, micro_step0
+        self.slots = slots
         self.K = gr.e.K
         gr.gs.copy_(gscale.reshape(()))
         self.steps = torch.arange(micro_step0, micro_step0 + len(mbs), dtype=torch.int64).to(
@@ -453,7 +460,7 @@ class _GraphRun:
         self.gbusy = [False] * self.K
 
     def _slot(self, i):
-        return self.gr.slots[i % self.K]
+        return self.slots[i % self.K]
 
     def x_buffer(self, i):
         k = i % self.K
@@ -516,7 +523,7 @@ class _GraphRun:
         self.gbusy[slot] = False
 
     def finish(self):
-        for sl in self.gr.slots:  # every send of this step has completed before the optimizer step
+        for sl in self.slots:  # every send of this step has completed before the optimizer step
             for key in ("send_y", "send_gx"):
                 if sl[key] is not None:
                     sl[key].wait()

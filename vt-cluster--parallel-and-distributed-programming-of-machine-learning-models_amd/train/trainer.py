@@ -254,7 +254,7 @@ class Trainer:
         reset_wgrads()  # a previous step's backward that raised must not leak queued weight grads
         ntok = self._global_tokens(mbs)
         if self.reducer is not None:
-            self.reducer.begin_step()
+            self.reducer.begin_step(self.global_step + 1)
         lr = self.sched(self.global_step)
         self.opt.set_lr(lr)
         if self.graphed is not None and self.graphed.supported(mbs):
@@ -299,6 +299,7 @@ class Trainer:
             if self._comm_ev is None:
                 self._comm_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self._comm_ev[0].record()
+        maybe_inject(self.rank, self.global_step + 1, "grads", grads=self.arena.grad)
         with rng("mift.comm.grads"):
             if self.zero:
                 self.opt.reduce_grads()

@@ -22,7 +22,7 @@ def parse(spec: str):
     return (None if parts[0] == "*" else int(parts[0])), int(parts[1]), parts[2], where
 
 
-def maybe_inject(rank: int, step: int, where: str = "step"):
+def maybe_inject(rank: int, step: int, where: str = "step", grads=None):
     spec = os.environ.get("MIFT_FAULT")
     if not spec:
         return
@@ -30,8 +30,13 @@ def maybe_inject(rank: int, step: int, where: str = "step"):
     r, s, kind, w = parse(spec)
     if _fired or (r is not None and r != rank) or s != step or w != where:
         return
+    if kind == "inf" and grads is None:
+        return
     _fired = True  # once per process (several micro-batches share a step number)
     print(f"[FAULT] injecting {kind} on rank {rank} at step {step} ({where})", flush=True)
+    if kind == "inf":
+        grads.view(-1)[0] = float("inf")
+        return
     if kind == "raise":
         raise RuntimeError(f"injected fault on rank {rank} step {step}")
     if kind == "exit":
