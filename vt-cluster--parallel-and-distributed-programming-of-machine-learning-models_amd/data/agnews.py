@@ -144,11 +144,27 @@ def load_bert_tokenizer(path=None):
         if os.path.exists(os.path.join(path, "mift_tokenizer.txt")):
             return HashWordTokenizer()
         if BertTokenizerFast and os.path.exists(os.path.join(path, "vocab.txt")):
-            return BertTokenizerFast.from_pretrained(path)
+            return bert_tokenizer_from_vocab(os.path.join(path, "vocab.txt"), BertTokenizerFast)
     vocab = find_bert_vocab()
     if vocab and BertTokenizerFast:
-        return BertTokenizerFast(vocab_file=vocab, do_lower_case=True)
+        return bert_tokenizer_from_vocab(vocab, BertTokenizerFast)
     return HashWordTokenizer()
+
+
+def bert_tokenizer_from_vocab(path, cls=None):
+    """WordPiece tokenizer from a vocab.txt-format file (one token per line, id = line number).
+
+    The vocabulary is passed as a token -> id dict: transformers 5 ignores the vocab_file=
+    keyword of BertTokenizerFast and silently builds a 5-token (special tokens only) vocabulary,
+    which maps every word to [UNK] — the round-3 labs trained on all-[UNK] inputs and sat at chance."""
+    if cls is None:
+        from transformers import BertTokenizerFast as cls
+    with open(path, "r", encoding="utf-8") as f:
+        vocab = {ln.rstrip("\n"): i for i, ln in enumerate(f)}
+    tok = cls(vocab=vocab, do_lower_case=True)
+    if tok.vocab_size != len(vocab):
+        raise RuntimeError(f"WordPiece vocabulary from {path}: {tok.vocab_size} of {len(vocab)} tokens loaded")
+    return tok
 
 
 def encode(tok, texts, labels, seq_len=128):
