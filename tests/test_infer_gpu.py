@@ -115,3 +115,60 @@ def test_padded_distinct_prompts_match_solo_nocache(name):
         total += 8
     print(f"{name}: padded-batch vs solo no-cache token agreement {agree}/{total}")
     assert agree >= 0.95 * total, (agree, total)
+
+
+def test_decode_attn_device_position_matches_host():
+    """decode_attn with the position in an int32 device tensor (graph-replayed decode) == host int."""
+    from mift.ops import kernels as K
+    torch.manual_seed(2)
+    B, H, hd, Tmax, t = 2, 3, 64, 96, 70
+    dt = torch.bfloat16
+    kc = torch.randn(B, H, Tmax, hd, device="cuda").to(dt)
+    vc = torch.randn(B, H, Tmax, hd, device="cuda").to(dt)
+    qkv = torch.randn(B, 3 * H * hd, device="cuda").to(dt)
+    plen = torch.tensor([9, 31], device="cuda", dtype=torch.int32)
+    k1, v1, k2, v2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    o1 = K.decode_attn(qkv, k1, v1, t, hd ** -0.5, plen=plen, gend=40)
+    o2 = K.decode_attn(qkv, k2, v2, torch.tensor([t], dtype=torch.int32, device="cuda"), hd ** -0.5, plen=plen,
+                       gend=40)
+    assert torch.equal(o1, o2) and torch.equal(k1, k2) and torch.equal(v1, v2)
+
+
+@pytest.mark.parametrize("name", ["gpt2", "opt"])
+def test_graphed_decode_matches_eager(name, monkeypatch):
+    """Decode steps replayed from one hipGraph (device-side position / flags / output column) give the
+    eager loop's tokens exactly, for left-padded batches and with HF's stop-when-all-finished rule."""
+    from mift.apps.gen_probe import distinct_prompts
+    from mift.infer import generate as G
+    from mift.models.gpt2 import GPT2Config, GPT2LMHeadModel
+    from mift.models.opt import OPTConfig, OPTForCausalLM
+    if name == "gpt2":
+        m = GPT2LMHeadModel(GPT2Config(vocab_size=1000, n_positions=128, n_embd=128, n_layer=2, n_head=2,
+                                       n_inner=512), dtype=torch.bfloat16, device="cuda").init_weights(1)
+    else:
+        m = OPTForCausalLM(OPTConfig(vocab_size=1000, hidden_size=320, num_hidden_layers=2, ffn_dim=1280,
+                                     num_attention_heads=4, max_position_embeddings=128), dtype=torch.float16,
+                           device="cuda").init_weights(2)
+    m.eval()
+    ids, mask = distinct_prompts(16, 1000, 1, "cuda")
+
+    def both(**kw):
+        monkeypatch.setenv("MIFT_GEN_GRAPH", "0")
+        e = G.generate(m, ids, attention_mask=mask, **kw)
+        monkeypatch.setenv("MIFT_GEN_GRAPH", "1")
+        g1 = G.generate(m, ids, attention_mask=mask, **kw)  # captures
+        g2 = G.generate(m, ids, attention_mask=mask, **kw)  # replays the cached graph
+        return e, g1, g2
+
+    e, g1, g2 = both(max_new_tokens=12, eos_token_id=-1)
+    assert e.shape == (16, ids.shape[1] + 12) and torch.equal(e, g1) and torch.equal(e, g2)
+    # early stop: identical prompts -> identical rows; EOS := the 4th generated token
+    same = ids[:1].expand(4, -1).contiguous()
+    msk = mask[:1].expand(4, -1).contiguous()
+    monkeypatch.setenv("MIFT_GEN_GRAPH", "0")
+    ref_out = G.generate(m, same, attention_mask=msk, max_new_tokens=12, eos_token_id=-1)
+    eos = int(ref_out[0, same.shape[1] + 3])
+    e = G.generate(m, same, attention_mask=msk, max_new_tokens=12, eos_token_id=eos)
+    monkeypatch.setenv("MIFT_GEN_GRAPH", "1")
+    g = G.generate(m, same, attention_mask=msk, max_new_tokens=12, eos_token_id=eos)
+    assert e.shape[1] <= same.shape[1] + 4 and torch.equal(e, g), (e.shape, g.shape)

@@ -27,7 +27,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ 
                                                           T* __restrict__ vc, T* __restrict__ out,
                                                           const int* __restrict__ start,
                                                           const int* __restrict__ plen, int gend, int H, int Tmax,
-                                                          int t, float scale) {
+                                                          int t_arg, const int* __restrict__ t_dev, float scale) {
+  // t_dev: the position lives on the device (graph-replayed decode steps advance it in-graph)
+  const int t = t_dev ? t_dev[0] : t_arg;
   constexpr int G = 256 / HD;  // key groups in the P·V pass
   extern __shared__ float sm[];
   float* qs = sm;              // [HD]
@@ -103,26 +105,37 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ 
 
 template <typename T, int HD>
 void launch(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, at::Tensor& out, const int* start, const int* plen,
-            int gend, int B, int H, int Tmax, int t, float scale, hipStream_t st) {
+            int gend, int B, int H, int Tmax, int t, const int* t_dev, float scale, hipStream_t st) {
   constexpr int G = 256 / HD;
-  const size_t smem = (size_t)(HD + G * HD + t + 1) * sizeof(float);
+  // score buffer for keys [0, t]; a device-side t is only bounded by the cache
+  const size_t smem = (size_t)(HD + G * HD + (t_dev ? Tmax : t + 1)) * sizeof(float);
   hipLaunchKernelGGL((decode_attn_kernel<T, HD>), dim3(B * H), dim3(256), smem, st, (const T*)qkv.data_ptr(),
-                     (T*)kc.data_ptr(), (T*)vc.data_ptr(), (T*)out.data_ptr(), start, plen, gend, H, Tmax, t, scale);
+                     (T*)kc.data_ptr(), (T*)vc.data_ptr(), (T*)out.data_ptr(), start, plen, gend, H, Tmax, t, t_dev,
+                     scale);
 }
 
 }  // namespace
 
 // qkv [B, 3*H*HD]; kc/vc [B, H, Tmax, HD] (row t written); start [B] int32 or None; plen [B] int32 or
-// None with gend: keys in [plen[b], gend) masked -> o [B, H*HD]
+// None with gend: keys in [plen[b], gend) masked -> o [B, H*HD].  t_dev: optional int32 [1] device
+// tensor holding the position (t is then only the host-side lower bound; the caller keeps
+// gend <= t_dev < Tmax — graph-replayed decode steps advance it in-graph, infer/generate.py).
 at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
                             const c10::optional<at::Tensor>& start, const c10::optional<at::Tensor>& plen,
-                            int64_t gend) {
+                            int64_t gend, const c10::optional<at::Tensor>& t_dev) {
   TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 2, "decode_attn: qkv [B, 3*H*HD] contiguous");
   TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.sizes() == vc.sizes(),
               "decode_attn: caches [B,H,Tmax,HD]");
   TORCH_CHECK(kc.scalar_type() == qkv.scalar_type() && vc.scalar_type() == qkv.scalar_type(), "decode_attn: dtype");
   const int B = kc.size(0), H = kc.size(1), Tmax = kc.size(2), HD = kc.size(3);
   TORCH_CHECK(qkv.size(0) == B && qkv.size(1) == 3LL * H * HD, "decode_attn: qkv/cache shape mismatch");
+  const int* td = nullptr;
+  if (t_dev && t_dev->defined()) {
+    TORCH_CHECK(t_dev->is_cuda() && t_dev->scalar_type() == at::kInt && t_dev->numel() == 1,
+                "decode_attn: t_dev int32 [1] GPU tensor");
+    TORCH_CHECK(Tmax <= 16384, "decode_attn: cache too long for the LDS score buffer");
+    td = t_dev->data_ptr<int>();
+  }
   TORCH_CHECK(t >= 0 && t < Tmax, "decode_attn: position ", t, " outside cache of ", Tmax);
   TORCH_CHECK(t < 16384, "decode_attn: context too long for the LDS score buffer");
   const int* sp = nullptr;
@@ -142,8 +155,8 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
   TORCH_CHECK(half || qkv.scalar_type() == at::kBFloat16, "decode_attn: bf16/fp16");
 #define MIFT_DEC(D)                                                                        \
   case D:                                                                                  \
-    if (half) launch<fp16, D>(qkv, kc, vc, out, sp, pl, (int)gend, B, H, Tmax, (int)t, (float)scale, st); \
-    else launch<bf16, D>(qkv, kc, vc, out, sp, pl, (int)gend, B, H, Tmax, (int)t, (float)scale, st);      \
+    if (half) launch<fp16, D>(qkv, kc, vc, out, sp, pl, (int)gend, B, H, Tmax, (int)t, td, (float)scale, st); \
+    else launch<bf16, D>(qkv, kc, vc, out, sp, pl, (int)gend, B, H, Tmax, (int)t, td, (float)scale, st);      \
     break;
   switch (HD) {
     MIFT_DEC(32) MIFT_DEC(64) MIFT_DEC(80) MIFT_DEC(128)

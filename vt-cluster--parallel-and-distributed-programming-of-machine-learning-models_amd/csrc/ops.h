@@ -86,7 +86,7 @@ at::Tensor mift_attn_bwd_bits(const at::Tensor& dout, const at::Tensor& qkv, con
 // ---- K12 decode attention over a KV cache (kernels/decode.hip)
 at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
                             const c10::optional<at::Tensor>& start, const c10::optional<at::Tensor>& plen,
-                            int64_t gend);
+                            int64_t gend, const c10::optional<at::Tensor>& t_dev);
 
 #define MIFT_BIND_MORE(m) \
   m.def("decode_attn", &mift_decode_attn, "single-token attention over a KV cache; appends k/v at t (left padding: start; prompt gap: plen, gend)"); \

@@ -16,6 +16,15 @@ the ``decode_attn`` HIP kernel, which appends the new K/V in the same
 launch, and the LM-head logits are the hand-written MFMA GEMM (``gemm_nt``).
 No library GEMM and no SDPA run on the GPU path.
 
+Decode steps are replayed from ONE hipGraph (``_DecodeGraph``; ``MIFT_GEN_GRAPH=0`` disables): a
+step is ~45 kernels of a few microseconds each, so eagerly it was host-launch bound (0.62 ms per
+step for distilgpt2 at batch 64).  Everything a step varies lives on the
+device — the cache position (``decode_attn`` reads it from an int32 tensor), the positions, the
+finished-row flags and the output column — and advances inside the graph, so one capture serves
+every step and, cached per (model, batch, prompt length, budget), every later call of the same
+shape.  HF's stop-when-all-finished rule is applied afterwards: the steps past the last row's EOS
+only produce pad tokens and are trimmed (no per-step host sync).
+
 Left-padded batches: the prefill runs every prompt RIGHT-aligned to position 0
 (row b's tokens ``ids[b, start_b:]`` then padding) so the flash kernel's
 ``kv_len`` key mask is exact — queries see keys [0, q] of their own prompt,
@@ -25,6 +34,9 @@ prompt at [0, len_b) and generated tokens from S0 on; the decode kernel masks
 the gap [len_b, S0).  Returned ids keep the HF left-padded layout.  CPU
 tensors run the same algorithm with torch ops (the oracle).
 """
+import gc
+import os
+
 import torch
 
 from ..ops import reference as ref
@@ -112,6 +124,76 @@ def _heads(model):
     return a.n_head, a.head_dim
 
 
+class _DecodeGraph:
+    """One captured greedy decode step over static device state (see the module docstring)."""
+
+    def __init__(self, model, B, S0, max_new, H, hd, padded, fill, pad, eos, dtype, dev):
+        self.key = (B, S0, max_new, padded, pad, eos, fill)
+        L = len(model.blocks())
+        self.cache = KVCache(L, B, H, S0 + max_new, hd, dtype, dev)
+        self.B, self.S0, self.H, self.hd, self.fill, self.pad, self.eos = B, S0, H, hd, fill, pad, eos
+        self.nxt = torch.zeros(B, dtype=torch.long, device=dev)
+        self.done = torch.zeros(B, dtype=torch.bool, device=dev)
+        self.t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.pos = torch.zeros(B, 1, dtype=torch.long, device=dev)
+        self.col = torch.zeros(B, 1, dtype=torch.long, device=dev)
+        self.out = torch.zeros(B, max_new, dtype=torch.long, device=dev)
+        self.plen = torch.zeros(B, dtype=torch.int32, device=dev) if padded else None
+        self.graph = None
+
+    def step(self, model):
+        """One decode step on the static state (eager, or recorded during capture)."""
+        B, H, hd = self.B, self.H, self.hd
+        ids = torch.where(self.done, torch.full_like(self.nxt, self.fill), self.nxt)[:, None]
+        h = model.embed_at(ids, self.pos)
+        h = _run_blocks(model, h, lambda li: _decode_attn(self.cache, li, B, H, hd, self.t, self.plen, self.S0, True),
+                        True)
+        nx = model.head_logits(h)[:, -1].float().argmax(-1)
+        nx = torch.where(self.done, torch.full_like(nx, self.pad), nx)
+        self.out.scatter_(1, self.col, nx[:, None])
+        if self.eos is not None:
+            self.done |= nx == self.eos
+        self.nxt.copy_(nx)
+        self.t += 1
+        self.pos += 1
+        self.col += 1
+
+    def run(self, model, nsteps):
+        if nsteps <= 0:
+            return
+        i = 0
+        if self.graph is None:
+            self.step(model)  # eager warm-up (first launch of every kernel module), then capture
+            i = 1
+            if nsteps > 1:
+                g = torch.cuda.CUDAGraph()
+                was = gc.isenabled()
+                gc.collect()
+                gc.disable()  # no finalizers of device objects inside the capture (train/graph.py)
+                try:
+                    with torch.cuda.graph(g):
+                        self.step(model)
+                finally:
+                    if was:
+                        gc.enable()
+                self.graph = g
+        for _ in range(i, nsteps):
+            self.graph.replay()
+
+
+_GRAPHS = {}
+
+
+def _decode_graph(model, key_args):
+    key = (id(model),) + tuple(key_args[:10])
+    g = _GRAPHS.get(key)
+    if g is None:
+        if len(_GRAPHS) >= 4:
+            _GRAPHS.pop(next(iter(_GRAPHS)))
+        g = _GRAPHS[key] = _DecodeGraph(model, *key_args)
+    return g
+
+
 @torch.no_grad()
 def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token_id=None, pad_token_id=None,
              max_length=None):
@@ -138,16 +220,25 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
     H, hd = _heads(model)
     L = len(model.blocks())
     dtype = model.tied_embedding().dtype
-    cache = KVCache(L, B, H, S0 + max_new_tokens, hd, dtype, dev)
+    vocab = model.tied_embedding().shape[0]
+    fill = pad if pad is not None and 0 <= pad < vocab else 0
+    dg = None
+    if (fused and dev.type == "cuda" and max_new_tokens > 2 and os.environ.get("MIFT_GEN_GRAPH", "1") != "0"
+            and S0 + max_new_tokens <= 16384):
+        dg = _decode_graph(model, (B, S0, max_new_tokens, padded, pad, eos, fill, H, hd, dtype, dev))
+        cache = dg.cache
+        if padded:
+            dg.plen.copy_(plen)
+            plen = dg.plen
+    else:
+        cache = KVCache(L, B, H, S0 + max_new_tokens, hd, dtype, dev)
 
     # prefill over right-aligned prompts: row b = ids[b, start_b:] then padding, positions 0..S0-1
     ar = torch.arange(S0, device=dev)
-    # filler after each right-aligned prompt / input of a finished row: any id INSIDE the embedding
-    # table.  Filler K/V are masked (kv_len, the decode gap) but still multiplied by p = 0 inside the
-    # kernels' P·V, so an out-of-table id (GPT-2's pad = eos = 50256 on a smaller test vocabulary)
-    # read garbage rows and a non-finite V turned 0·V into NaN for the whole row.
-    vocab = model.tied_embedding().shape[0]
-    fill = pad if pad is not None and 0 <= pad < vocab else 0
+    # filler after each right-aligned prompt / input of a finished row (``fill`` above): any id INSIDE
+    # the embedding table.  Filler K/V are masked (kv_len, the decode gap) but still multiplied by
+    # p = 0 inside the kernels' P·V, so an out-of-table id (GPT-2's pad = eos = 50256 on a smaller test
+    # vocabulary) read garbage rows and a non-finite V turned 0·V into NaN for the whole row.
     if padded:
         src = (ar[None, :] + start[:, None]).clamp(max=S0 - 1)
         ids_r = torch.where(ar[None, :] < lens[:, None], torch.gather(input_ids, 1, src),
@@ -160,6 +251,8 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
     h_last = torch.gather(h, 1, last[:, None, None].expand(B, 1, h.shape[-1])) if padded else h[:, -1:]
     logits = model.head_logits(h_last)
     nxt = logits[:, -1].float().argmax(-1)
+    if dg is not None:
+        return _graphed_decode(dg, model, input_ids, nxt, lens, max_new_tokens, pad, eos)
     out = [input_ids]
     done = torch.zeros(B, dtype=torch.bool, device=dev)
     for i in range(max_new_tokens):
@@ -175,6 +268,28 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
         h = _run_blocks(model, h, lambda li: _decode_attn(cache, li, B, H, hd, t, plen, S0, fused), fused)
         nxt = model.head_logits(h)[:, -1].float().argmax(-1)
     return torch.cat(out, 1)
+
+
+def _graphed_decode(dg, model, input_ids, nxt, lens, max_new_tokens, pad, eos):
+    """Token 0 from the prefill, tokens 1.. from graph replays; HF's early stop applied afterwards."""
+    done = torch.zeros_like(dg.done) if eos is None else (nxt == eos)
+    dg.nxt.copy_(nxt)
+    dg.done.copy_(done)
+    dg.out.zero_()
+    dg.out[:, 0] = nxt
+    dg.t.fill_(dg.S0)
+    dg.pos.copy_(lens[:, None])
+    dg.col.fill_(1)
+    dg.run(model, max_new_tokens - 1)
+    toks = dg.out.clone()
+    if eos is not None:
+        # HF stops after the step in which the last unfinished row emitted EOS
+        hit = toks == eos
+        if bool(hit.any(1).all()):
+            first = torch.where(hit, torch.arange(max_new_tokens, device=toks.device)[None, :],
+                                max_new_tokens).min(1).values
+            toks = toks[:, :int(first.max()) + 1]
+    return torch.cat([input_ids, toks], 1)
 
 
 @torch.no_grad()

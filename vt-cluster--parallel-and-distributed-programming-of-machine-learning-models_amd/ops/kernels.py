@@ -98,8 +98,11 @@ def xent(logits, labels, V, ignore_index=-100, write_grad=True):
 
 def decode_attn(qkv, kcache, vcache, t, scale, start=None, plen=None, gend=0):
     """o [B, H*hd] for the token at position t; writes its k/v into the caches.  Masked keys:
-    ``< start[b]`` (left padding) and ``[plen[b], gend)`` (right-aligned prompts, generate.py)."""
-    return C().decode_attn(qkv, kcache, vcache, int(t), float(scale), start, plen, int(gend))
+    ``< start[b]`` (left padding) and ``[plen[b], gend)`` (right-aligned prompts, generate.py).
+    ``t`` may be an int32 [1] device tensor (graph-replayed decode: the position advances in-graph)."""
+    if isinstance(t, torch.Tensor):
+        return C().decode_attn(qkv, kcache, vcache, int(gend), float(scale), start, plen, int(gend), t)
+    return C().decode_attn(qkv, kcache, vcache, int(t), float(scale), start, plen, int(gend), None)
 
 
 def layer_norm_fwd_proj(x, w, b, eps, pw, rank, alpha=1.0, p=0.0, seed=0):
