@@ -123,11 +123,24 @@ def bench_epi_ab(results):
         results.append(row)
 
 
-def bench_dgpt(results):
+def opt_m_cases(Ms=(2048, 4096, 24576)):
+    """OPT-2.7B layer GEMMs (with their training epilogues) at the micro-batch sizes of the PP configs:
+    M = mb x 512 tokens (mb 4 / 8 / 48)."""
+    base = [("opt.qkv.fwd+ext+bias", 7680, 2560, dict(bias=1, ext=1)),
+            ("opt.out.fwd+ext+drop+res", 2560, 2560, dict(bias=1, ext=1, p=0.1, res=1)),
+            ("opt.fc1.fwd+ext+relu", 10240, 2560, dict(bias=1, ext=1, act=2)),
+            ("opt.fc2.fwd+ext+drop+res", 2560, 10240, dict(bias=1, ext=1, p=0.1, res=1)),
+            ("opt.fc2.dgrad+maskext+relubwd", 10240, 2560, dict(ext=1, ext_p=0.05, act=5, aux=1)),
+            ("opt.fc1.dgrad+maskext", 2560, 10240, dict(ext=1, ext_p=0.05)),
+            ("opt.out.dgrad+maskext", 2560, 2560, dict(ext=1, ext_p=0.05)),
+            ("opt.qkv.dgrad+maskext", 2560, 7680, dict(ext=1, ext_p=0.05))]
+    return [(f"{n}@M{M}", M, N, K, e) for M in Ms for n, N, K, e in base]
+
+
+def bench_dgpt(results, cases=None, dt=torch.bfloat16):
     import mift._C as C
-    dt = torch.bfloat16
     tot = {}
-    for name, M, N, K, e in DGPT_CASES:
+    for name, M, N, K, e in cases or DGPT_CASES:
         a = torch.randn(M, K, device="cuda", dtype=dt)
         b = torch.randn(N, K, device="cuda", dtype=dt) / K ** 0.5
         bias = torch.randn(N, device="cuda", dtype=dt) if e.get("bias") else None
@@ -146,6 +159,7 @@ def bench_dgpt(results):
         print(json.dumps(row), flush=True)
         results.append(row)
     print("per-layer total us by tile:", json.dumps({k: round(v, 1) for k, v in tot.items()}), flush=True)
+    return tot
 
 
 def bench_ln(results):
@@ -172,7 +186,9 @@ def main():
     results = []
     for k in a.only.split(","):
         {"gemm": bench_gemm, "ln": bench_ln, "dgpt": bench_dgpt, "epi": bench_epi_ab,
-         "opt": lambda r: bench_gemm(r, OPT_SHAPES, torch.float16)}[k](results)
+         "opt": lambda r: bench_gemm(r, OPT_SHAPES, torch.float16),
+         "optm": lambda r: bench_dgpt(r, opt_m_cases(), torch.float16),
+         "optm_small": lambda r: bench_dgpt(r, opt_m_cases((2048, 4096)), torch.float16)}[k](results)
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
         with open(a.json, "w") as f:
