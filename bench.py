@@ -82,7 +82,9 @@ def parse_args(argv=None):
                          "lines (README.md:66: ~20k) sharded over the DP ranks and report its wall clock "
                          "(the reference's [Training] sec metric); default 20000 for GPT-2, 0 (skip) for OPT")
     a = ap.parse_args(argv)
-    c = CONFIGS[a.config]
+    c = dict(CONFIGS[a.config])
+    if a.model and a.model != c["model"]:  # a model override keeps that family's reference precision
+        c["precision"] = "fp16" if "opt" in a.model.lower() else "bf16"
     a.model = a.model or c["model"]
     a.gpus = a.gpus if a.gpus is not None else c["gpus"]
     a.pp = a.pp if a.pp is not None else c["pp"]
@@ -182,7 +184,7 @@ def main():
 
     def sync():
         if on_gpu:
-            sync()
+            torch.cuda.synchronize()
 
     split = None
     kw = {}

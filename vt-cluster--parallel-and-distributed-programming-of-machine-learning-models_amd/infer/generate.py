@@ -127,7 +127,7 @@ def _heads(model):
 class _DecodeGraph:
     """One captured greedy decode step over static device state (see the module docstring)."""
 
-    def __init__(self, model, B, S0, max_new, H, hd, padded, fill, pad, eos, dtype, dev):
+    def __init__(self, model, B, S0, max_new, padded, pad, eos, fill, H, hd, dtype, dev):
         self.key = (B, S0, max_new, padded, pad, eos, fill)
         L = len(model.blocks())
         self.cache = KVCache(L, B, H, S0 + max_new, hd, dtype, dev)

@@ -26,11 +26,11 @@ import math
 GiB = 1 << 30
 
 # ms per sequence of a whole dp1 optimizer step (all layers + embed + head + optimizer), seq 512,
-# 96 sequences per step, fp16, fused HIP path, graph replay: tools/mb_sweep.py on one MI355X.
-# Source: profiles/r4/mb_sweep_*.jsonl (filled from the GPU sweep; the r3 pair for OPT-2.7B is
-# mb 4 -> 1132 ms / 96 and mb 48 -> 642 ms / 96, profiles/r3/rehearse_opt27b_pp4.json).
+# 96 sequences per step, fp16, fused HIP path, graph replay: tools/mb_sweep.py on one MI355X
+# (profiles/r4/mb_sweep_opt27b.jsonl, mb_sweep_opt67b.jsonl; round 4, before the small-M kernel work).
 MEASURED = {
-    "opt-2.7b": {4: 11.79, 48: 6.69},
+    "opt-2.7b": {1: 25.5406, 2: 14.4509, 4: 11.2882, 8: 7.9349, 12: 6.9053, 16: 7.4457, 24: 6.6494, 48: 6.5463},
+    "opt-6.7b": {1: 34.2091, 2: 20.8388, 4: 18.9054, 8: 14.9082, 16: 14.7781, 32: 14.7251},
 }
 
 LINK_BW = 100e9        # bytes/s one xGMI link achieves for a large RCCL p2p (≈153 GB/s raw)

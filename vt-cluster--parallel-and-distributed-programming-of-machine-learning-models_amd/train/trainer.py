@@ -62,6 +62,7 @@ class TrainConfig:
     logging_first_step: bool = False
     graph: str = "auto"                # hipGraph-replayed steps (mift.train.graph): auto | on | off (MIFT_GRAPH)
     consistency_every: int = 0         # >0: checksum the trainable params across DP replicas every N steps
+    consistency_rtol: float = 1e-5     # periodic check: ulp-level drift tolerated (and healed), see verify_replicas
     max_inflight_steps: int = 2        # host run-ahead bound (GPU): wait for step i-N before returning from step i
     profile_dir: Optional[str] = None  # torch.profiler window (mift.obs.profiler): trace/kernels/ranges per rank
     profile_steps: str = "3:6"         # global steps [A, B) recorded when profile_dir is set
@@ -362,7 +363,7 @@ class Trainer:
                         print(lab_step_line(self.rank, self.global_step, dt * 1000, sps, sps * seq), flush=True)
                 self._tok_seen += sum(int(mb["input_ids"].numel()) for mb in mbs) * self.dp
                 if cfg.consistency_every and self.dp > 1 and self.global_step % cfg.consistency_every == 0:
-                    verify_replicas([self.arena.param], group=self.dp_group)
+                    verify_replicas([self.arena.param], group=self.dp_group, rtol=cfg.consistency_rtol, resync=True)
                 if log_now:
                     self._perf_log(mbs)
                     st = self.opt.stats()
