@@ -70,6 +70,9 @@ def parse_args(argv=None):
                     help="regroup batch*accum into micro-batches of this size; 'auto' (PP default): "
                          "mift.parallel.plan's HBM-bounded cost model")
     ap.add_argument("--pp", type=int, default=None, help="pipeline stages (world = dp x pp)")
+    ap.add_argument("--virtual_stages", dest="virtual", default=None,
+                    help="interleaved 1F1B model chunks per pipeline rank; 'auto' (PP default): chosen with the "
+                         "micro-batch by mift.parallel.plan")
     ap.add_argument("--partition", default="balanced", choices=["uniform", "balanced"])
     ap.add_argument("--zero", type=int, default=0)
     ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "fp32"],
@@ -97,6 +100,8 @@ def parse_args(argv=None):
         a.epoch_lines = c.get("epoch_lines", 0 if "opt" in a.model.lower() else 20000)
     if a.micro_batch == "0" and a.pp > 1:
         a.micro_batch = "auto"
+    if a.virtual is None:
+        a.virtual = "auto" if (a.pp > 1 and a.micro_batch == "auto") else "1"
     return a
 
 
@@ -168,7 +173,21 @@ def main():
     is_opt = "opt" in a.model.lower()
     a.seq_len = a.seq_len or (512 if is_opt else 256)
     a.accum = a.accum or (96 if is_opt else 32)
-    ctx = D.init(pp=a.pp, verbose=False, sanity=True)
+    from mift.models.opt import OPTConfig
+    from mift.models.gpt2 import GPT2Config
+    mcfg = OPTConfig.preset(a.model) if is_opt else GPT2Config.preset(a.model)
+    per_rank = a.batch * a.accum
+    plan = None
+    if a.pp > 1 and (a.micro_batch == "auto" or a.virtual == "auto"):
+        # micro-batch and interleaving depth from the measured dp1 cost curve (before the grid is built:
+        # interleaving needs the wrap-around links)
+        from mift.parallel.plan import choose_micro_batch
+        cands = None if a.micro_batch == "auto" else [int(a.micro_batch)]
+        plan = choose_micro_batch(mcfg, a.seq_len, per_rank, a.pp, dtype_bytes=2, name=a.model, candidates=cands,
+                                  virtual="auto" if a.virtual == "auto" else int(a.virtual))
+        a.micro_batch, a.virtual = str(plan["micro_batch"]), str(plan["virtual"])
+    V = int(a.virtual)
+    ctx = D.init(pp=a.pp, verbose=False, sanity=True, virtual=V)
     n = ctx.world
     if n != a.gpus or ctx.pp != a.pp:
         fail(f"formed world {n} (pp {ctx.pp}) differs from --gpus {a.gpus} --pp {a.pp}")
@@ -188,13 +207,11 @@ def main():
 
     split = None
     kw = {}
-    from mift.models.opt import OPTConfig
-    from mift.models.gpt2 import GPT2Config
-    mcfg = OPTConfig.preset(a.model) if is_opt else GPT2Config.preset(a.model)
     if ctx.pp > 1:
-        from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
-        split = partition_layers(mcfg.num_layers(), ctx.pp, a.partition, head_cost_layers(mcfg))
-        kw = dict(layer_range=stage_layer_range(split, ctx.pp_rank), has_embed=ctx.is_first_stage,
+        from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_chunks
+        split = partition_layers(mcfg.num_layers(), ctx.pp * V, a.partition, head_cost_layers(mcfg), ranks=ctx.pp)
+        chunks = stage_chunks(split, ctx.pp, V, ctx.pp_rank)
+        kw = dict(layer_range=chunks if V > 1 else chunks[0], has_embed=ctx.is_first_stage,
                   has_head=ctx.is_last_stage)
     model = build_causal_lm(a.model, dtype=dtype, device=ctx.device, seed=0, **kw)
     targets = ["q_proj", "k_proj", "v_proj", "out_proj", "fc1", "fc2"] if is_opt else ["c_attn", "c_proj"]
@@ -202,13 +219,7 @@ def main():
                                  base_model_name_or_path=a.model))
     if a.impl == "torch":
         model.fused = False
-    per_rank = a.batch * a.accum
-    plan = None
-    if a.micro_batch == "auto" and ctx.pp > 1:
-        from mift.parallel.plan import choose_micro_batch
-        plan = choose_micro_batch(mcfg, a.seq_len, per_rank, ctx.pp, dtype_bytes=dtype.itemsize, name=a.model)
-        mb, acc = plan["micro_batch"], per_rank // plan["micro_batch"]
-    elif a.micro_batch not in ("0", "auto") and per_rank % int(a.micro_batch) == 0:
+    if a.micro_batch not in ("0", "auto") and per_rank % int(a.micro_batch) == 0:
         mb, acc = int(a.micro_batch), per_rank // int(a.micro_batch)
     else:
         mb, acc = (per_rank, 1) if (a.fold_accum and ctx.pp == 1) else (a.batch, a.accum)
@@ -309,7 +320,8 @@ def main():
         sync()
         setup_s = round(time.perf_counter() - ts, 4)
         epoch_s, epoch_steps = timed_epoch(tr2)
-    par = f"dp{ctx.dp}" + (f"xpp{ctx.pp}" if ctx.pp > 1 else "") + ("+zero1" if a.zero and ctx.dp > 1 else "")
+    par = (f"dp{ctx.dp}" + (f"xpp{ctx.pp}" if ctx.pp > 1 else "") + (f"xv{V}" if V > 1 else "")
+           + ("+zero1" if a.zero and ctx.dp > 1 else ""))
     if ctx.rank == 0:
         kind = "PP" if ctx.pp > 1 else "DDP"
         out = {

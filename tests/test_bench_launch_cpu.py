@@ -71,3 +71,13 @@ def test_bench_no_gpu_fails_loudly():
 def test_bench_bad_pipeline_grid_fails():
     out = _run(["--gpus", "2", "--config", "3"] + SMALL)
     assert out.returncode != 0 and "pipeline stages" in out.stderr
+
+
+def test_bench_interleaved_pipeline_grid():
+    """--virtual_stages 2: two model chunks per pipeline rank (interleaved 1F1B over the wrap-around link)."""
+    out = _run(["--gpus", "2", "--config", "3", "--pp", "2", "--virtual_stages", "2", "--micro_batch", "2",
+                "--model", "opt-tiny", "--precision", "fp32", "--seq_len", "32", "--accum", "4"] + SMALL)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = _json(out)
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp1xpp2xv2"
+    assert r["config"]["split"] == [1, 1, 1, 1] and r["value"] > 0

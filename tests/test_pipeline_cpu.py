@@ -14,7 +14,7 @@ from mift.utils import harness
 
 
 def _worker(rank, world, pp=1, zero=0, steps=2, mb=2, accum=4, dropout=0.0, partition="uniform",
-            ckpt_dir=None, resume=None, p2p="link"):
+            ckpt_dir=None, resume=None, p2p="link", virtual=1):
     import os
     os.environ["MIFT_PP_P2P"] = p2p
     from mift import lora as L
@@ -22,13 +22,13 @@ def _worker(rank, world, pp=1, zero=0, steps=2, mb=2, accum=4, dropout=0.0, part
     from mift.models import build_causal_lm
     from mift.models.opt import OPTConfig
     from mift.parallel import dist as D
-    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
+    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_chunks, stage_layer_range
     from mift.train.trainer import TrainConfig, Trainer
 
-    ctx = D.init(pp=pp, verbose=False, sanity=True)
+    ctx = D.init(pp=pp, verbose=False, sanity=True, virtual=virtual)
     cfg = OPTConfig.preset("opt-tiny")
-    split = partition_layers(cfg.num_hidden_layers, ctx.pp, partition, head_cost_layers(cfg))
-    lr_ = stage_layer_range(split, ctx.pp_rank)
+    split = partition_layers(cfg.num_hidden_layers, ctx.pp * virtual, partition, head_cost_layers(cfg))
+    lr_ = stage_layer_range(split, ctx.pp_rank) if virtual == 1 else stage_chunks(split, ctx.pp, virtual, ctx.pp_rank)
     model = build_causal_lm("opt-tiny", seed=3, layer_range=lr_, has_embed=ctx.is_first_stage,
                             has_head=ctx.is_last_stage)
     model.config.dropout = dropout
@@ -127,6 +127,36 @@ def test_pp_checkpoint_resume(tmp_path, single_drop):
     r = harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, steps=2, ckpt_dir=d, resume="auto")
     for k in single_drop["state"]:
         torch.testing.assert_close(r[0]["state"][k], single_drop["state"][k], atol=2e-5, rtol=1e-4)
+
+
+def test_interleaved_pipeline_matches_single(single_drop):
+    """Interleaved 1F1B (2 ranks x 2 model chunks = 4 virtual stages of one layer each, the wrap-around
+    links carry chunk 0's activations from rank 1 back to chunk 1 on rank 0) reproduces the
+    single-process run with dropout on; adapters gathered from both chunks of both ranks."""
+    r = harness.run(_worker, 2, pp=2, dropout=0.1, virtual=2)
+    _close_runs(r[0], single_drop)
+
+
+def test_interleaved_dp_x_pp(single):
+    """2 DP replicas x 2 interleaved pipeline ranks (V = 2) == single process."""
+    r = harness.run(_worker, 4, pp=2, virtual=2)
+    _close_runs(r[0], single)
+
+
+def test_interleaved_schedule_is_deadlock_free():
+    """Blocking receives + asynchronous sends (the engine's execution model) complete every
+    interleaved schedule: every rank count, chunk count and micro-batch count tried."""
+    from mift.parallel.pipeline import schedule_interleaved, simulate_schedule
+    for S in (2, 3, 4, 8):
+        for V in (1, 2, 4):
+            for M in (S, 2 * S, 4 * S):
+                assert simulate_schedule(S, M, V) == 2 * S * M * V, (S, M, V)
+    # every rank runs each (chunk, micro-batch) forward and backward exactly once
+    ops = schedule_interleaved(4, 1, 8, 2)
+    assert sorted(o for o in ops if o[0] == "F") == sorted(("F", c, i) for c in range(2) for i in range(8))
+    assert sorted(o for o in ops if o[0] == "B") == sorted(("B", c, i) for c in range(2) for i in range(8))
+    with pytest.raises(ValueError):
+        schedule_interleaved(4, 0, 6, 2)  # micro-batches must be a multiple of the stages
 
 
 def test_1f1b_schedule_order():

@@ -39,7 +39,7 @@ from ..data.tokenizer import load_tokenizer
 from ..models import build_causal_lm
 from ..obs.timing import PhaseLogger, p2_loss_line
 from ..parallel import dist as D
-from ..parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
+from ..parallel.pipeline import head_cost_layers, partition_layers, stage_chunks, stage_layer_range
 from ..train.trainer import TrainConfig, Trainer
 
 
@@ -57,6 +57,8 @@ def build_argparser():
     ap.add_argument("--ds_cfg", default="deepspeed_pp_zero1_cpu.json")
     # mift extensions
     ap.add_argument("--pp", type=int, default=None, help="pipeline stages (default $PIPELINE_PARALLEL_SIZE or world)")
+    ap.add_argument("--virtual_stages", type=int, default=None,
+                    help="interleaved 1F1B: model chunks per pipeline rank (default $PIPELINE_VIRTUAL_STAGES or 1)")
     ap.add_argument("--partition", choices=["uniform", "balanced"], default=None,
                     help="layer split (default: mift.pp_partition / pipeline.partition_method, else balanced)")
     ap.add_argument("--precision", choices=["fp16", "bf16", "fp32"], default=None)
@@ -95,7 +97,7 @@ def main(argv=None):
     world_env = int(os.environ.get("WORLD_SIZE", os.environ.get("SLURM_NTASKS", "1")))
     stages = args.pp or int(os.environ.get("PIPELINE_PARALLEL_SIZE", str(world_env)))
     assert 1 <= stages <= 32, "PIPELINE_PARALLEL_SIZE must be in [1,32]"
-    ctx = D.init(pp=stages)
+    ctx = D.init(pp=stages, virtual=args.virtual_stages)
     rank = ctx.rank
 
     def log(msg):
@@ -131,16 +133,19 @@ def main(argv=None):
     from ..models.opt import OPTConfig
     cfg = OPTConfig.preset(args.model_name)
     N = cfg.num_hidden_layers
-    split = partition_layers(N, ctx.pp, args.partition or ds.pp_partition, head_cost_layers(cfg))
-    lo, hi = stage_layer_range(split, ctx.pp_rank)
+    V = ctx.pp_virtual
+    split = partition_layers(N, ctx.pp * V, args.partition or ds.pp_partition, head_cost_layers(cfg), ranks=ctx.pp)
+    mine = stage_chunks(split, ctx.pp, V, ctx.pp_rank)  # V == 1: one contiguous range
+    lo, hi = mine[0][0], mine[-1][1]
     model = build_causal_lm(args.model_name, dtype=dtype, device=ctx.device, seed=args.seed,
-                            weights=args.base_weights, layer_range=(lo, hi), has_embed=ctx.is_first_stage,
-                            has_head=ctx.is_last_stage)
+                            weights=args.base_weights, layer_range=mine if V > 1 else mine[0],
+                            has_embed=ctx.is_first_stage, has_head=ctx.is_last_stage)
     lcfg = L.LoraConfig(r=args.lora_r, lora_alpha=args.lora_alpha, lora_dropout=args.lora_dropout,
                         target_modules=args.target_modules.split(","), base_model_name_or_path=args.model_name)
     L.inject(model, lcfg, seed=args.seed)
     model.seed = args.seed
-    log(f"Pipeline split={split} (total blocks={N}, stages={ctx.pp}) -> my layers [{lo},{hi})")
+    log(f"Pipeline split={split} (total blocks={N}, stages={ctx.pp}"
+        + (f", {V} interleaved chunks per stage) -> my chunks {mine}" if V > 1 else f") -> my layers [{lo},{hi})"))
     logs.log("Model build", time.perf_counter() - t0, echo=False)
 
     # ---- tokenization ----
@@ -207,7 +212,7 @@ def main(argv=None):
         if tok is not None:
             tok.save_pretrained(out)
         with open(os.path.join(out, "meta.json"), "w") as f:
-            json.dump({"split": split, "stages": ctx.pp}, f, indent=2)
+            json.dump({"split": split, "stages": ctx.pp, "virtual_stages": ctx.pp_virtual}, f, indent=2)
         log(f"Saved adapters+tokenizer to {out}")
     logs.log("Model save", time.perf_counter() - t0, echo=False)
     tokens = trainer.global_step * per_step * args.seq_len * ctx.dp

@@ -8,6 +8,10 @@ the pipeline engine and the generator treat them alike:
     on a stage without a head (``layer_range`` / ``has_embed`` / ``has_head``
     build only one pipeline stage's weights: SURVEY §6 — the reference OOMs
     because every rank materialises the whole fp32 model first);
+  * interleaved pipeline stages (``parallel/pipeline.py``, virtual stages): ``layer_range`` may
+    be a LIST of (lo, hi) chunks; the pipeline engine selects one with ``active_chunk`` before a
+    forward, which then runs only that chunk's blocks, the embedding only on the first chunk of the
+    first stage and the head only on the last chunk of the last stage;
   * ``seed`` / ``micro_step``: counter-based dropout seeds, so a block
     recomputed under activation checkpointing — or re-run by the pipeline
     engine's backward — draws bit-identical masks;
@@ -21,7 +25,41 @@ from ..ops.dispatch import use_kernels
 from .layers import dropout_seed, seed_for
 
 
+def normalize_chunks(layer_range, n_layers):
+    """``layer_range``: None (all layers), (lo, hi), or [(lo, hi), ...] (interleaved chunks)
+    -> (span (lo, hi), chunk list, per-layer membership)"""
+    if layer_range is None:
+        chunks = [(0, n_layers)]
+    elif isinstance(layer_range[0], (tuple, list)):
+        chunks = [tuple(c) for c in layer_range]
+    else:
+        chunks = [tuple(layer_range)]
+    for lo, hi in chunks:
+        if not (0 <= lo < hi <= n_layers):
+            raise ValueError(f"bad layer chunk {(lo, hi)} for {n_layers} layers")
+    member = [any(lo <= i < hi for lo, hi in chunks) for i in range(n_layers)]
+    return (min(c[0] for c in chunks), max(c[1] for c in chunks)), chunks, member
+
+
 class CausalLMBase(nn.Module):
+    active_chunk = None  # interleaved pipeline: index into chunk_ranges run by forward (None: all)
+
+    def blocks(self):
+        """The decoder blocks this module runs: all of its blocks, or those of ``active_chunk``."""
+        bl = self.all_blocks()
+        if self.active_chunk is None:
+            return bl
+        lo, hi = self.chunk_ranges[self.active_chunk]
+        return [b for b in bl if lo <= b.idx < hi]
+
+    @property
+    def embed_here(self):
+        return self.has_embed and self.active_chunk in (None, 0)
+
+    @property
+    def head_here(self):
+        return self.has_head and self.active_chunk in (None, len(self.chunk_ranges) - 1)
+
     def _init_runtime(self, vocab_padded):
         self.vocab_padded = vocab_padded
         self.seed = 0

@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import reference as ref
-from .base import CausalLMBase, ref_lm_loss
+from .base import CausalLMBase, normalize_chunks, ref_lm_loss
 from .layers import Embedding, LayerNorm, Linear, dropout_seed, init_normal_, padded_vocab, seed_for
 
 
@@ -153,7 +153,7 @@ class GPT2LMHeadModel(CausalLMBase):
         self.config = cfg
         self.dtype_ = dtype
         n = cfg.n_layer
-        self.layer_range = layer_range or (0, n)
+        self.layer_range, self.chunk_ranges, member = normalize_chunks(layer_range, n)
         self.has_embed, self.has_head = has_embed, has_head
         self.vocab_padded = padded_vocab(cfg.vocab_size)
         self.transformer = nn.Module()
@@ -162,8 +162,7 @@ class GPT2LMHeadModel(CausalLMBase):
         if has_embed:
             self.transformer.wpe = Embedding(cfg.n_positions, cfg.n_embd, dtype=dtype, device=device)
         self.transformer.h = nn.ModuleList(
-            [GPT2Block(cfg, i, dtype, device) if self.layer_range[0] <= i < self.layer_range[1] else nn.Identity()
-             for i in range(n)])
+            [GPT2Block(cfg, i, dtype, device) if member[i] else nn.Identity() for i in range(n)])
         if has_head:
             self.transformer.ln_f = LayerNorm(cfg.n_embd, cfg.layer_norm_epsilon, dtype=dtype, device=device)
         self._init_runtime(self.vocab_padded)
@@ -174,7 +173,7 @@ class GPT2LMHeadModel(CausalLMBase):
         init_normal_(self, std, proj_std=std / (2 * self.config.n_layer) ** 0.5, seed=seed)
         return self
 
-    def blocks(self):
+    def all_blocks(self):
         return [b for b in self.transformer.h if isinstance(b, GPT2Block)]
 
     def tied_embedding(self):
@@ -209,7 +208,7 @@ class GPT2LMHeadModel(CausalLMBase):
             from .gpt2_fused import fused_forward
             return fused_forward(self, input_ids, attention_mask, labels, hidden_states, reduction, return_logits)
         key_valid = None
-        h = self.embed_ref(input_ids, attention_mask) if self.has_embed else hidden_states
+        h = self.embed_ref(input_ids, attention_mask) if self.embed_here else hidden_states
         for blk in self.blocks():
             seeds = blk.site_seeds(self.seed, self.micro_step)
             if self.recompute and self.training:
@@ -217,7 +216,7 @@ class GPT2LMHeadModel(CausalLMBase):
                                                       use_reentrant=False)
             else:
                 h = blk.forward_ref(h, seeds, self.training, key_valid)
-        if not self.has_head:
+        if not self.head_here:
             return {"hidden_states": h}
         loss, logits = self.head_ref(h, labels, reduction)
         return {"loss": loss, "logits": logits if return_logits else None}

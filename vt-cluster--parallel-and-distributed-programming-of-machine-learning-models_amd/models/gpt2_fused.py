@@ -21,7 +21,7 @@ def block_forward(blk, h, seeds, training, kv_len=None):
 def fused_forward(model, input_ids, attention_mask, labels, hidden_states, reduction, return_logits):
     cfg = model.config
     training = model.training
-    if model.has_embed:
+    if model.embed_here:
         B, S = input_ids.shape
         wte = model.transformer.wte.weight
         h = K.embed(input_ids.contiguous(), wte, model.transformer.wpe.weight,
@@ -35,7 +35,7 @@ def fused_forward(model, input_ids, attention_mask, labels, hidden_states, reduc
             h = torch.utils.checkpoint.checkpoint(blk.forward_fused, h, seeds, training, use_reentrant=False)
         else:
             h = blk.forward_fused(h, seeds, training)
-    if not model.has_head:
+    if not model.head_here:
         return {"hidden_states": h}
     w_nk, w_kn = model.lm_weight_padded(transposed=labels is not None and torch.is_grad_enabled())
     if labels is not None:

@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import reference as ref
-from .base import CausalLMBase, ref_lm_loss, shift_labels
+from .base import CausalLMBase, normalize_chunks, ref_lm_loss, shift_labels
 from .layers import ConcatLinear, Embedding, LayerNorm, Linear, dropout_seed, init_normal_, padded_vocab, seed_for
 
 
@@ -200,7 +200,7 @@ class OPTForCausalLM(CausalLMBase):
         self.config = cfg
         self.dtype_ = dtype
         n = cfg.num_hidden_layers
-        self.layer_range = layer_range or (0, n)
+        self.layer_range, self.chunk_ranges, member = normalize_chunks(layer_range, n)
         self.has_embed, self.has_head = has_embed, has_head
         d = cfg.hidden_size
         self.model = nn.Module()
@@ -210,8 +210,7 @@ class OPTForCausalLM(CausalLMBase):
         if has_embed:
             dec.embed_positions = OPTLearnedPositionalEmbedding(cfg.max_position_embeddings, d, dtype, device)
         dec.layers = nn.ModuleList(
-            [OPTDecoderLayer(cfg, i, dtype, device) if self.layer_range[0] <= i < self.layer_range[1]
-             else nn.Identity() for i in range(n)])
+            [OPTDecoderLayer(cfg, i, dtype, device) if member[i] else nn.Identity() for i in range(n)])
         if has_head:
             dec.final_layer_norm = LayerNorm(d, cfg.layer_norm_eps, dtype=dtype, device=device)
         self._init_runtime(padded_vocab(cfg.vocab_size))
@@ -231,7 +230,7 @@ class OPTForCausalLM(CausalLMBase):
     def final_norm(self):
         return self.model.decoder.final_layer_norm
 
-    def blocks(self):
+    def all_blocks(self):
         return [b for b in self.model.decoder.layers if isinstance(b, OPTDecoderLayer)]
 
     # ---- pieces ----
@@ -256,7 +255,7 @@ class OPTForCausalLM(CausalLMBase):
         if self._use_fused(ref_in):
             return self._forward_fused(input_ids, attention_mask, labels, hidden_states, reduction, ignore_index)
         key_valid = attention_mask.bool() if attention_mask is not None else None
-        h = self.embed_ref(input_ids, attention_mask) if self.has_embed else hidden_states
+        h = self.embed_ref(input_ids, attention_mask) if self.embed_here else hidden_states
         for blk in self.blocks():
             seeds = blk.site_seeds(self.seed, self.micro_step)
             if self.recompute and self.training and torch.is_grad_enabled():
@@ -264,7 +263,7 @@ class OPTForCausalLM(CausalLMBase):
                                                       use_reentrant=False)
             else:
                 h = blk.forward_ref(h, seeds, self.training, key_valid)
-        if not self.has_head:
+        if not self.head_here:
             return {"hidden_states": h}
         loss, logits = self.head_ref(h, labels, reduction, ignore_index)
         out = {"loss": loss, "logits": logits if return_logits else None}
@@ -278,7 +277,7 @@ class OPTForCausalLM(CausalLMBase):
         cfg, training = self.config, self.training
         dec = self.model.decoder
         kv_len = attention_mask.sum(1, dtype=torch.int32) if attention_mask is not None else None
-        if self.has_embed:
+        if self.embed_here:
             B, S = input_ids.shape
             pos = opt_positions(attention_mask).contiguous() if attention_mask is not None else None
             h = K.embed(input_ids.contiguous(), dec.embed_tokens.weight, dec.embed_positions.weight, pos=pos,
@@ -292,7 +291,7 @@ class OPTForCausalLM(CausalLMBase):
                                                       use_reentrant=False)
             else:
                 h = blk.forward_fused(h, seeds, training, kv_len)
-        if not self.has_head:
+        if not self.head_here:
             return {"hidden_states": h}
         w_nk, w_kn = self.lm_weight_padded(transposed=labels is not None and torch.is_grad_enabled())
         if labels is not None:

@@ -79,6 +79,12 @@ class DistContext:
     # link_*[0] is the link to the previous stage, link_*[1] to the next (None at the ends)
     link_f: List[Optional[object]] = field(default_factory=lambda: [None, None])  # activations s -> s+1
     link_b: List[Optional[object]] = field(default_factory=lambda: [None, None])  # grads s+1 -> s
+    # interleaved pipeline (pp_virtual > 1 model chunks per rank): the wrap-around pair (last stage,
+    # first stage) carries chunk c's activations from the last stage to chunk c+1 on the first stage
+    # (wrap_f) and the matching gradients back (wrap_b)
+    pp_virtual: int = 1
+    wrap_f: Optional[object] = None
+    wrap_b: Optional[object] = None
 
     @property
     def is_main(self):
@@ -110,11 +116,12 @@ def want_gpu() -> bool:
 
 
 def init(pp: Optional[int] = None, backend: Optional[str] = None, timeout_s: Optional[int] = None,
-         sanity: bool = True, verbose: bool = True) -> DistContext:
+         sanity: bool = True, verbose: bool = True, virtual: Optional[int] = None) -> DistContext:
     """Initialise the process group (idempotent) and build the DP×PP grid.
 
     ``pp`` defaults to $PIPELINE_PARALLEL_SIZE or 1.  Ranks are laid out
-    pipeline-major: replica r owns ranks [r*pp, (r+1)*pp).
+    pipeline-major: replica r owns ranks [r*pp, (r+1)*pp).  ``virtual`` (default
+    $PIPELINE_VIRTUAL_STAGES or 1): model chunks per pipeline rank (interleaved 1F1B).
     """
     global _CTX
     if _CTX is not None:
@@ -153,7 +160,10 @@ def init(pp: Optional[int] = None, backend: Optional[str] = None, timeout_s: Opt
     if pp < 1 or world % pp != 0:
         raise ValueError(f"pipeline size {pp} must divide world size {world}")
     ctx.timeout = timeout
-    build_grid(ctx, pp)
+    virtual = virtual or int(os.environ.get("PIPELINE_VIRTUAL_STAGES", "1") or 1)
+    if virtual < 1:
+        raise ValueError(f"virtual pipeline stages {virtual} < 1")
+    build_grid(ctx, pp, virtual)
     _CTX = ctx
     if verbose:
         print(f"[RANK {rank}] WORLD_SIZE={world}", flush=True)
@@ -167,10 +177,11 @@ def init(pp: Optional[int] = None, backend: Optional[str] = None, timeout_s: Opt
     return ctx
 
 
-def build_grid(ctx: DistContext, pp: int):
+def build_grid(ctx: DistContext, pp: int, virtual: int = 1):
     world = ctx.world
     dp = world // pp
     ctx.dp, ctx.pp = dp, pp
+    ctx.pp_virtual = virtual if pp > 1 else 1
     ctx.dp_rank, ctx.pp_rank = ctx.rank // pp, ctx.rank % pp
     # every rank must create every group in the same order
     for r in range(dp):
@@ -194,6 +205,12 @@ def build_grid(ctx: DistContext, pp: int):
                 ctx.link_f[1], ctx.link_b[1] = lf, lb
             elif ctx.rank == pair[1]:
                 ctx.link_f[0], ctx.link_b[0] = lf, lb
+        if multi and ctx.pp_virtual > 1:
+            pair = [ranks[0], ranks[-1]]
+            wf = dist.new_group(pair, timeout=ctx.timeout)
+            wb = dist.new_group(pair, timeout=ctx.timeout)
+            if ctx.rank in pair:
+                ctx.wrap_f, ctx.wrap_b = wf, wb
     for s in range(pp):
         ranks = list(range(s, world, pp))
         g = dist.new_group(ranks, timeout=ctx.timeout) if dp > 1 and world > 1 else None

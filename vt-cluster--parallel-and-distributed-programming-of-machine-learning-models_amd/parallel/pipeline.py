@@ -45,6 +45,22 @@ design that also fixes its defects:
     that read it.  OPT-2.7B at the reference's micro-batch issues ~250 launches per micro-batch
     from Python eagerly; a replay is one launch.
 
+Interleaved 1F1B (``ctx.pp_virtual`` = V > 1, Narayanan et al. 2021 / Megatron-LM's
+interleaved schedule): the layers are split into S·V virtual stages and rank s holds chunks
+s, S + s, 2S + s, ... (``stage_chunks``), so a micro-batch visits every rank V times and the
+bubble shrinks from (S−1)/(M+S−1) to (S−1)/(V·M+S−1) at the same micro-batch size — on MI355X
+that is the lever: small micro-batches leave the matrix cores idle (tools/mb_sweep.py: OPT-2.7B
+costs 1.7× per token at 4 sequences per micro-batch vs 48), so the pipeline wants FEW, LARGE
+micro-batches, and the interleaving pays for the bubble that creates.  Activations of chunk c
+leave the last rank for chunk c+1 on the first rank over a wrap-around pair of 2-rank
+communicators (``ctx.wrap_f`` / ``ctx.wrap_b``); every communicator still carries one message
+kind between one sender and one receiver in an order both agree on (the k-th forward of every
+rank is the same (chunk, micro-batch), see ``schedule_interleaved``), receives are posted one op
+ahead into fresh buffers and waited right before their consumer, sends are asynchronous — a
+blocking-receive / async-send execution of this schedule is deadlock-free
+(tests/test_pipeline_cpu.py simulates it for every rank count tried).  The interleaved path runs
+eagerly (no stage graphs).
+
 Loss normalisation: the last stage scales each micro-batch's summed token
 loss by ``loss_scale / global_ntokens`` (token-count normalisation over the
 whole optimizer step and all DP replicas), so PP, DP and single-GPU runs
@@ -59,12 +75,28 @@ import torch
 from .comm import P2P
 
 
-def partition_layers(n_layers, n_stages, method="uniform", head_layers=0.0, embed_layers=0.0):
-    """-> list of per-stage layer counts (sum = n_layers)."""
+def partition_layers(n_layers, n_stages, method="uniform", head_layers=0.0, embed_layers=0.0, ranks=None):
+    """-> list of per-stage layer counts (sum = n_layers).
+
+    ``ranks`` (interleaved pipeline, n_stages = ranks x chunks): "balanced" then balances the per-RANK
+    sums (virtual stage k runs on rank k % ranks): equal chunks, the last chunk (which carries the
+    head) shortened by the head's layer-equivalents, the removed layers spread over the other
+    ranks' chunks from the front."""
     if n_stages > n_layers:
         raise ValueError(f"{n_stages} stages > {n_layers} layers")
     if method == "uniform":
         return [n_layers // n_stages + (1 if i < n_layers % n_stages else 0) for i in range(n_stages)]
+    if method == "balanced" and ranks and ranks > 1 and n_stages > ranks:
+        split = [n_layers // n_stages + (1 if i < n_layers % n_stages else 0) for i in range(n_stages)]
+        take = min(int(head_layers + 0.5), split[-1] - 1)
+        split[-1] -= take
+        k = 0
+        while take > 0:  # round-robin over the chunks not on the last rank
+            if k % ranks != ranks - 1:
+                split[k] += 1
+                take -= 1
+            k = (k + 1) % (n_stages - 1)
+        return split
     if method != "balanced":
         raise ValueError(method)
     # minimise the max stage cost; cost(stage) = layers + embed (first) + head (last)
@@ -104,6 +136,69 @@ def stage_layer_range(split, stage):
     return lo, lo + split[stage]
 
 
+def stage_chunks(split, stages, virtual, stage):
+    """Layer ranges held by pipeline rank ``stage`` when ``split`` partitions the layers over
+    ``stages * virtual`` virtual stages: chunk c = virtual stage c·stages + stage."""
+    if len(split) != stages * virtual:
+        raise ValueError(f"split over {len(split)} virtual stages, expected {stages} x {virtual}")
+    return [stage_layer_range(split, c * stages + stage) for c in range(virtual)]
+
+
+def schedule_interleaved(S, s, M, V):
+    """Op order of rank s in the interleaved 1F1B schedule: [('F' | 'B', chunk, micro-batch)].
+
+    The k-th forward of EVERY rank is chunk (k mod S·V) // S of micro-batch (k // S·V)·S + k mod S;
+    the k-th backward the same with the chunk order reversed.  Rank s runs
+    min(2(S−s−1) + (V−1)·S, M·V) warm-up forwards (all of them when M == S), then one forward /
+    one backward, then the remaining backwards.  Needs M % S == 0."""
+    if V == 1:
+        return [(op, 0, i) for op, i in schedule_1f1b(S, s, M)]
+    if M % S:
+        raise ValueError(f"interleaved schedule: {M} micro-batches is not a multiple of {S} stages")
+    total = M * V
+
+    def fwd(k):
+        return (k % (S * V)) // S, (k // (S * V)) * S + k % S
+
+    def bwd(k):
+        c, i = fwd(k)
+        return V - 1 - c, i
+
+    nwarm = total if M == S else min(2 * (S - s - 1) + (V - 1) * S, total)
+    ops = [("F",) + fwd(k) for k in range(nwarm)]
+    for j in range(total - nwarm):
+        ops.append(("F",) + fwd(nwarm + j))
+        ops.append(("B",) + bwd(j))
+    ops += [("B",) + bwd(k) for k in range(total - nwarm, total)]
+    return ops
+
+
+def simulate_schedule(S, M, V):
+    """Execute every rank's op list with blocking receives and asynchronous sends; returns the
+    number of ops run (== 2·S·M·V when the schedule cannot deadlock)."""
+    ops = [schedule_interleaved(S, s, M, V) if V > 1 else [(o, 0, i) for o, i in schedule_1f1b(S, s, M)]
+           for s in range(S)]
+    done, pos, ran = set(), [0] * S, 0
+    progress = True
+    while progress:
+        progress = False
+        for s in range(S):
+            while pos[s] < len(ops[s]):
+                op, c, i = ops[s][pos[s]]
+                vs = c * S + s
+                if op == "F":
+                    ok = vs == 0 or ("F", vs - 1, i) in done
+                else:
+                    ok = ("F", vs, i) in done and (vs == S * V - 1 or ("B", vs + 1, i) in done)
+                if not ok:
+                    break
+                done.add((op, vs, i))
+                pos[s] += 1
+                ran += 1
+                progress = True
+    return ran
+
+
 def head_cost_layers(cfg):
     """LM-head MACs in units of one decoder layer (12·d² MACs per token + attention ignored)."""
     d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd")
@@ -135,6 +230,15 @@ class PipelineEngine:
         else:
             raise ValueError(f"MIFT_PP_P2P={self.mode!r}: link | shared | blocking")
         self.blocking = self.mode == "blocking"
+        self.V = getattr(ctx, "pp_virtual", 1) or 1
+        if self.V > 1:
+            self.rx_wf, self.tx_wf = P2P(getattr(ctx, "wrap_f", None)), P2P(getattr(ctx, "wrap_f", None))
+            self.rx_wb, self.tx_wb = P2P(getattr(ctx, "wrap_b", None)), P2P(getattr(ctx, "wrap_b", None))
+            self.first_rank, self.last_rank = ctx.pp_ranks[0], ctx.pp_ranks[-1]
+            if len(getattr(model, "chunk_ranges", [])) != self.V:
+                raise ValueError(f"interleaved pipeline: the stage model holds "
+                                 f"{len(getattr(model, 'chunk_ranges', []))} chunks, expected {self.V}")
+            graph = False  # the interleaved schedule runs eagerly
         self.dtype, self.d = act_dtype, hidden_size
         self.device = ctx.device
         self.stats = {"fwd": 0, "bwd": 0, "replays": 0}
@@ -153,11 +257,12 @@ class PipelineEngine:
     def _forward(self, mb, x, micro_step):
         m = self.model
         m.micro_step = micro_step
-        out = m(input_ids=mb["input_ids"] if self.first else None, attention_mask=mb["attention_mask"],
-                labels=mb["labels"] if self.last else None, hidden_states=x, reduction="sum",
+        emb, head = getattr(m, "embed_here", self.first), getattr(m, "head_here", self.last)  # chunk-aware
+        out = m(input_ids=mb["input_ids"] if emb else None, attention_mask=mb["attention_mask"],
+                labels=mb["labels"] if head else None, hidden_states=x, reduction="sum",
                 return_logits=False)
         self.stats["fwd"] += 1
-        return out["loss"].float() if self.last else out["hidden_states"]
+        return out["loss"].float() if head else out["hidden_states"]
 
     def _backward(self, y, x, grad_y, gscale):
         if self.last:
@@ -186,11 +291,88 @@ class PipelineEngine:
         into a reusable ring buffer.  On RCCL ``Pending.wait()`` only orders the compute
         stream behind the transfer, so the host never blocks and xGMI transfers overlap the
         forward / backward kernels."""
+        if self.V > 1:
+            return self._schedule_interleaved(mbs, gscale, micro_step0)
         if self.graphs is not None:
             run = self.graphs.runner(mbs, gscale, micro_step0)
             if run is not None:
                 return self._schedule(mbs, run)
         return self._schedule(mbs, _EagerRun(self, mbs, gscale, micro_step0))
+
+    # ---- interleaved 1F1B (V model chunks per rank) ----
+    def _schedule_interleaved(self, mbs, gscale, micro_step0):
+        S, s, V, M = self.S, self.s, self.V, len(mbs)
+        ops = schedule_interleaved(S, s, M, V)
+        nvs = S * V
+        m = self.model
+        loss = torch.zeros((), dtype=torch.float32, device=self.device) if self.last else None
+        live, posted, sends = {}, {}, []
+
+        def vstage(c):
+            return c * S + s
+
+        def needs_recv(j):
+            if j >= len(ops):
+                return None
+            op, c, i = ops[j]
+            vs = vstage(c)
+            if op == "F" and vs > 0:
+                return op, c, i
+            if op == "B" and vs < nvs - 1:
+                return op, c, i
+            return None
+
+        def post(key):
+            op, c, i = key
+            buf = torch.empty(self._act_shape(mbs[i]), dtype=self.dtype, device=self.device)
+            if op == "F":  # activation of virtual stage vs - 1
+                p2p, src = (self.rx_f, self.prev) if s > 0 else (self.rx_wf, self.last_rank)
+            else:          # gradient from virtual stage vs + 1
+                p2p, src = (self.rx_b, self.next) if s < S - 1 else (self.rx_wb, self.first_rank)
+            posted[key] = (self._post(p2p, recvs=[(buf, src)]), buf)
+
+        def take(key):
+            if key not in posted:
+                post(key)
+            pend, buf = posted.pop(key)
+            pend.wait()
+            return buf
+
+        try:
+            for j, (op, c, i) in enumerate(ops):
+                key = needs_recv(j)
+                if key is not None and key not in posted:
+                    post(key)
+                nxt = needs_recv(j + 1)  # one op of receive prefetch
+                if nxt is not None and nxt not in posted:
+                    post(nxt)
+                vs = vstage(c)
+                m.active_chunk = c
+                if op == "F":
+                    x = take(("F", c, i)).requires_grad_(True) if vs > 0 else None
+                    y = self._forward(mbs[i], x, micro_step0 + i)
+                    if vs == nvs - 1:
+                        loss.add_(y.detach())
+                    else:
+                        p2p, dst = (self.tx_f, self.next) if s < S - 1 else (self.tx_wf, self.first_rank)
+                        sends.append(self._post(p2p, sends=[(y.detach(), dst)]))
+                    live[(c, i)] = (x, y)
+                else:
+                    x, y = live.pop((c, i))
+                    g = take(("B", c, i)) if vs < nvs - 1 else None
+                    if vs == nvs - 1:
+                        (y * gscale).backward()
+                    else:
+                        torch.autograd.backward(y, grad_tensors=g)
+                    self.stats["bwd"] += 1
+                    if vs > 0:
+                        p2p, dst = (self.tx_b, self.prev) if s > 0 else (self.tx_wb, self.last_rank)
+                        sends.append(self._post(p2p, sends=[(x.grad, dst)]))
+        finally:
+            m.active_chunk = None
+        for p in sends:
+            p.wait()
+        return loss
 
     def _schedule(self, mbs, run):
         M = len(mbs)

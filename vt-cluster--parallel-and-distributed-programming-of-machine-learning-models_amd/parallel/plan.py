@@ -20,6 +20,13 @@ on top of its weights; candidates that do not fit ``hbm_budget`` are dropped.
 ``choose_micro_batch`` returns the fastest feasible mb together with the prediction, including
 the per-GPU efficiency against the best dp1 micro-batch (one GPU, no bubble), so a run records
 WHY it used the micro-batch it used.
+
+Interleaved 1F1B (``virtual`` V model chunks per rank, parallel/pipeline.py) cuts the bubble term
+to (S − 1)/V stage-times: step(mb, V) ≈ (m + (S − 1)/V) · T_stage(mb) + 2 (S·V − 1)/S · hop(mb)
+(every micro-batch now crosses S·V − 1 stage boundaries, spread over S ranks).  It needs
+m % S == 0 and S·V ≤ layers; ``choose_micro_batch(..., virtual="auto")`` searches (mb, V) jointly.
+The memory bound grows with the deeper warm-up: rank 0 keeps up to 2(S − 1) + (V − 1)·S + 1
+chunk-micro-batches of L/(S·V) layers alive.
 """
 import math
 
@@ -70,28 +77,40 @@ def _divisors(n):
     return [d for d in range(1, n + 1) if n % d == 0]
 
 
-def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_bytes=2, name=None):
-    """Predicted step time and per-GPU efficiency of an S-stage pipeline at micro-batch ``mb``."""
+def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_bytes=2, name=None, virtual=1,
+            op_overhead_s=None):
+    """Predicted step time and per-GPU efficiency of an S-stage pipeline at micro-batch ``mb``
+    (``virtual`` > 1: interleaved schedule with that many model chunks per rank).
+
+    Work is counted in layer-equivalents: a decoder layer is 1, the LM head V/(12 d) (on the last
+    virtual stage), the partition is ``partition_layers(..., "balanced")`` over S·V virtual stages
+    (or ``split``).  With u(mb) = dp1 time per layer-equivalent per micro-batch:
+        step ≈ m·max_rank_units·u + (S − 1)·max_chunk_units·u + m·V·op_overhead + hops
+    (the steady state runs at the slowest rank; warm-up and cool-down traverse the pipeline one
+    chunk at a time).  ``op_overhead``: fixed cost per chunk-micro-batch (fwd + bwd): p2p latency and
+    host launches — 20 µs graph-replayed (V = 1), 60 µs eager (V > 1)."""
+    from .pipeline import partition_layers
     name = name or getattr(cfg, "name_or_path", None) or "opt-2.7b"
     L = cfg.num_layers() if hasattr(cfg, "num_layers") else cfg.num_hidden_layers
     d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd")
     m = per_replica // mb
-    seq_ms = cost_per_seq_ms(name, mb, measured)          # whole model, dp1, per sequence
-    # stage share: the balanced partition equalises layers + head (the head ≈ V/(12 d) layers)
+    v = max(1, int(virtual))
+    nvs = stages * v
     head_layers = cfg.vocab_size / (12.0 * d)
     if split is None:
-        t_stage_frac = (L + head_layers) / stages / (L + head_layers)
-    else:
-        costs = [n + (head_layers if i == len(split) - 1 else 0.0) for i, n in enumerate(split)]
-        t_stage_frac = max(costs) / (L + head_layers)
-    t_stage = seq_ms * 1e-3 * mb * t_stage_frac
+        split = partition_layers(L, nvs, "balanced", head_layers, ranks=stages)
+    units = [n + (head_layers if k == nvs - 1 else 0.0) for k, n in enumerate(split)]
+    rank_units = [sum(units[c * stages + r] for c in range(v)) for r in range(stages)]
+    seq_ms = cost_per_seq_ms(name, mb, measured)          # whole model, dp1, per sequence
+    u = seq_ms * 1e-3 * mb / (L + head_layers)             # s per layer-equivalent per micro-batch
+    ovh = op_overhead_s if op_overhead_s is not None else (20e-6 if v == 1 else 60e-6)
     hop = mb * seq * d * dtype_bytes / LINK_BW + LINK_LAT
-    step = (m + stages - 1) * t_stage + 2 * (stages - 1) * hop
+    step = (m * max(rank_units) + (stages - 1) * max(units)) * u + m * v * ovh + 2 * (nvs - 1) / stages * hop
     best_dp1 = min(cost_per_seq_ms(name, x, measured) for x in _divisors(per_replica))
     dp1_step_per_gpu = best_dp1 * 1e-3 * per_replica / stages   # same work on S GPUs without a bubble
-    return {"micro_batch": mb, "micro_batches": m, "stage_ms": round(t_stage * 1e3, 3),
-            "hop_ms": round(hop * 1e3, 4), "step_ms": round(step * 1e3, 2),
-            "bubble": round((stages - 1) / (m + stages - 1), 4),
+    return {"micro_batch": mb, "micro_batches": m, "virtual": v, "split": list(split),
+            "stage_ms": round(max(rank_units) * u * 1e3, 3), "hop_ms": round(hop * 1e3, 4),
+            "step_ms": round(step * 1e3, 2), "bubble": round((stages - 1) / (v * m + stages - 1), 4),
             "efficiency_vs_dp1": round(dp1_step_per_gpu / step, 4)}
 
 
@@ -105,8 +124,9 @@ def act_bytes_per_token_layer(cfg, dtype_bytes=2):
 
 
 def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=288 * 10 ** 9,
-                       hbm_frac=0.85, measured=None, name=None, candidates=None):
-    """The feasible micro-batch (divisor of ``per_replica``) with the shortest predicted step."""
+                       hbm_frac=0.85, measured=None, name=None, candidates=None, virtual=1):
+    """The feasible micro-batch (divisor of ``per_replica``) with the shortest predicted step.
+    ``virtual``: model chunks per rank (int), or "auto" to choose among 1, 2, 4, ... as well."""
     L = cfg.num_layers() if hasattr(cfg, "num_layers") else cfg.num_hidden_layers
     n_params = getattr(cfg, "num_params", None)
     d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd")
@@ -114,20 +134,32 @@ def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=2
     layer_params = 4 * d * d + 2 * d * ffn
     weights = (layer_params * L / stages + cfg.vocab_size * d) * dtype_bytes
     budget = hbm_bytes * hbm_frac - weights
-    per_tok = act_bytes_per_token_layer(cfg, dtype_bytes) * math.ceil(L / stages)
+    if virtual == "auto":
+        vs = [v for v in (1, 2, 4) if stages > 1 and 2 * stages * v <= L] or [1]  # >= 2 layers per chunk
+    else:
+        vs = [int(virtual)]
     best, table = None, []
-    for mb in candidates or _divisors(per_replica):
-        need = stages * mb * seq * per_tok          # stage 0 holds S micro-batches in flight
-        p = predict(cfg, seq, per_replica, stages, mb, measured=measured, dtype_bytes=dtype_bytes, name=name)
-        p["act_gib"] = round(need / GiB, 2)
-        p["fits"] = need <= budget
-        table.append(p)
-        if p["fits"] and (best is None or p["step_ms"] < best["step_ms"]):
-            best = p
+    for v in vs:
+        per_tok = act_bytes_per_token_layer(cfg, dtype_bytes) * math.ceil(L / (stages * v))
+        for mb in candidates or _divisors(per_replica):
+            m = per_replica // mb
+            if v > 1 and m % stages:
+                continue
+            inflight = stages if v == 1 else min(2 * (stages - 1) + (v - 1) * stages + 1, m * v)
+            need = inflight * mb * seq * per_tok      # rank 0's live activations at the end of warm-up
+            p = predict(cfg, seq, per_replica, stages, mb, measured=measured, dtype_bytes=dtype_bytes, name=name,
+                        virtual=v)
+            p["act_gib"] = round(need / GiB, 2)
+            p["fits"] = need <= budget
+            table.append(p)
+            if p["fits"] and (best is None or p["step_ms"] < best["step_ms"] - 1e-9):
+                best = p
     if best is None:
         best = table[0]
     out = dict(best)
-    out["candidates"] = [{k: t[k] for k in ("micro_batch", "step_ms", "efficiency_vs_dp1", "fits")} for t in table]
-    out["model"] = "step = (m+S-1)*T_stage(mb) + 2(S-1)*hop; T_stage from the dp1 mb sweep"
+    out["candidates"] = [{k: t[k] for k in ("micro_batch", "virtual", "step_ms", "efficiency_vs_dp1", "fits")}
+                         for t in table]
+    out["model"] = ("step = (m*max_rank + (S-1)*max_chunk)*u(mb) + m*V*overhead + hops; u(mb) from the dp1 "
+                    "micro-batch sweep (profiles/r4/mb_sweep_*.jsonl)")
     del n_params
     return out
