@@ -12,7 +12,7 @@ GPU_ENV = {"MIFT_DEVICE": "cuda", "MIFT_BACKEND": "gloo"}
 
 
 def _worker(rank, world, pp=1, graph=False, steps=3, mb=2, accum=6, p2p="link", max_grad_norm=1.0,
-            consistency_every=0, zero=0):
+            consistency_every=0, zero=0, virtual=1):
     import os
     os.environ["MIFT_PP_P2P"] = p2p
     from mift import lora as L
@@ -20,15 +20,15 @@ def _worker(rank, world, pp=1, graph=False, steps=3, mb=2, accum=6, p2p="link", 
     from mift.models import build_causal_lm
     from mift.models.opt import OPTConfig
     from mift.parallel import dist as D
-    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
+    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_chunks, stage_layer_range
     from mift.train.trainer import TrainConfig, Trainer
 
-    ctx = D.init(pp=pp, verbose=False, sanity=True)
+    ctx = D.init(pp=pp, verbose=False, sanity=True, virtual=virtual)
     cfg = OPTConfig.preset("opt-tiny")
-    split = partition_layers(cfg.num_hidden_layers, ctx.pp, "uniform", head_cost_layers(cfg))
+    split = partition_layers(cfg.num_hidden_layers, ctx.pp * virtual, "uniform", head_cost_layers(cfg))
+    lr_ = stage_layer_range(split, ctx.pp_rank) if virtual == 1 else stage_chunks(split, ctx.pp, virtual, ctx.pp_rank)
     model = build_causal_lm("opt-tiny", dtype=torch.float16, device=ctx.device, seed=3,
-                            layer_range=stage_layer_range(split, ctx.pp_rank), has_embed=ctx.is_first_stage,
-                            has_head=ctx.is_last_stage)
+                            layer_range=lr_, has_embed=ctx.is_first_stage, has_head=ctx.is_last_stage)
     model.config.dropout = 0.1
     L.inject(model, L.LoraConfig(r=4, lora_alpha=8, lora_dropout=0.05,
                                  target_modules=["q_proj", "k_proj", "v_proj", "out_proj", "fc1", "fc2"]), seed=3)
@@ -38,7 +38,7 @@ def _worker(rank, world, pp=1, graph=False, steps=3, mb=2, accum=6, p2p="link", 
     batcher = MicroBatcher(ds, mb, accum, rank=ctx.dp_rank, world=ctx.dp)
     tc = TrainConfig(epochs=1, batch=mb, accum=accum, lr=1e-3, max_steps=steps, precision="fp16", logging_steps=1,
                      step_log="none", save_steps=0, graph="on" if graph else "off", max_grad_norm=max_grad_norm,
-                     consistency_every=consistency_every, zero_stage=zero)
+                     consistency_every=consistency_every, consistency_rtol=0.0, zero_stage=zero)
     tr = Trainer(model, batcher, tc, ctx)
     hist = tr.train()
     state = tr.adapter_state()
@@ -75,6 +75,14 @@ def test_pipeline_graphs_match_eager_and_single(single, pp):
         assert eager[r]["stats"]["replays"] == 0
     _close(eager[0], single, 2e-3)
     _close(graph[0], eager[0], 1e-3)
+
+
+def test_interleaved_pipeline_on_gpu(single):
+    """Interleaved 1F1B on the fused GPU kernels: 2 ranks x 2 model chunks (4 virtual stages of one
+    layer each; chunk 0's activations return from rank 1 to rank 0 over the wrap-around link),
+    eager, == the single-process run."""
+    r = harness.run(_worker, 2, env=GPU_ENV, timeout=240, pp=2, virtual=2)
+    _close(r[0], single, 2e-3)
 
 
 @pytest.mark.parametrize("p2p", ["shared", "blocking"])

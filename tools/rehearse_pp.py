@@ -23,24 +23,25 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def _worker(rank, world, model="facebook/opt-2.7b", pp=1, seq=512, mb=4, accum=24, steps=3, graph="auto",
-            partition="uniform"):
+            partition="uniform", virtual=1):
     import torch
     from mift import lora as L
     from mift.data import MicroBatcher, synthetic_openwebtext
     from mift.models import build_causal_lm
     from mift.models.opt import OPTConfig
     from mift.parallel import dist as D
-    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_layer_range
+    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_chunks
     from mift.train.trainer import TrainConfig, Trainer
 
-    ctx = D.init(pp=pp, verbose=False, sanity=True)
+    ctx = D.init(pp=pp, verbose=False, sanity=True, virtual=virtual)
     cfg = OPTConfig.preset(model)
     kw = {}
     split = None
     if ctx.pp > 1:
-        split = partition_layers(cfg.num_hidden_layers, ctx.pp, partition, head_cost_layers(cfg))
-        kw = dict(layer_range=stage_layer_range(split, ctx.pp_rank), has_embed=ctx.is_first_stage,
-                  has_head=ctx.is_last_stage)
+        V = ctx.pp_virtual
+        split = partition_layers(cfg.num_hidden_layers, ctx.pp * V, partition, head_cost_layers(cfg), ranks=ctx.pp)
+        ch = stage_chunks(split, ctx.pp, V, ctx.pp_rank)
+        kw = dict(layer_range=ch if V > 1 else ch[0], has_embed=ctx.is_first_stage, has_head=ctx.is_last_stage)
     m = build_causal_lm(model, dtype=torch.float16, device=ctx.device, seed=0, **kw)
     L.inject(m, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05,
                              target_modules=["q_proj", "k_proj", "v_proj", "out_proj", "fc1", "fc2"]))
@@ -81,13 +82,14 @@ def main():
     ap.add_argument("--accum", type=int, default=24)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--partition", default="uniform")
+    ap.add_argument("--virtual", type=int, default=1, help="interleaved 1F1B model chunks per pipeline rank")
     ap.add_argument("--skip_ref", action="store_true")
     ap.add_argument("--timeout", type=int, default=900)
     a = ap.parse_args()
     from mift.utils import harness
     env = {"MIFT_DEVICE": "cuda", "MIFT_BACKEND": "gloo", "OMP_NUM_THREADS": "2"}
     kw = dict(model=a.model, seq=a.seq, mb=a.mb, accum=a.accum, steps=a.steps, partition=a.partition)
-    out = {"model": a.model, "grid": f"dp{a.dp}xpp{a.pp}", "seq": a.seq, "micro_batch": f"{a.mb}x{a.accum}",
+    out = {"model": a.model, "grid": f"dp{a.dp}xpp{a.pp}" + (f"xv{a.virtual}" if a.virtual > 1 else ""), "seq": a.seq, "micro_batch": f"{a.mb}x{a.accum}",
            "transport": "gloo (one GPU, every rank its own process)"}
     t = time.perf_counter()
     if not a.skip_ref:
@@ -98,7 +100,7 @@ def main():
         print(f"dp{a.dp} reference done in {time.perf_counter() - t:.1f}s: {ref['loss']}", file=sys.stderr,
               flush=True)
     t = time.perf_counter()
-    res = harness.run(_worker, a.pp * a.dp, env=env, timeout=a.timeout, pp=a.pp, **kw)
+    res = harness.run(_worker, a.pp * a.dp, env=env, timeout=a.timeout, pp=a.pp, virtual=a.virtual, **kw)
     last = res[a.pp - 1]  # the last stage of replica 0 holds the loss; every rank logs the global one
     out["pp"] = {k: last[k] for k in ("loss", "grad_norm", "step_s", "split", "engine")}
     out["pp"]["max_mem_gib_per_rank"] = [r["max_mem_gib"] for r in res]
