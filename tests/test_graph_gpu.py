@@ -52,19 +52,18 @@ def test_graph_replay_matches_eager(name, precision, steps):
     le, pe, _, ge = _run(False, name, steps=steps, precision=precision)
     lg, pg, tr, gg = _run(True, name, steps=steps, precision=precision)
     assert tr.graphed is not None and len(tr.graphed.graphs) == 1, "graph was not captured"
-    assert le[0] == pytest.approx(lg[0], rel=1e-6, abs=1e-6)  # step 1 is the eager warm-up in both
-    for a, b in zip(le, lg):
-        assert a == pytest.approx(b, rel=1e-4, abs=1e-4), (le, lg)
-    for a, b in zip(ge, gg):
-        assert a == pytest.approx(b, rel=1e-2, abs=1e-5), (ge, gg)  # Adam-amplified atomics noise
+    # replay runs the eager step's kernels on the same operands in the same order (deterministic
+    # reductions, same dropout seeds, the same upstream scalar): bit-identical trajectories
+    # (tools/diag_graph_eager.py: max |dgrad| = max |dparam| = 0 over 20 distilgpt2 steps,
+    # profiles/r4/diag_graph_eager_distilgpt2_bf16_20steps.jsonl; OPT-125m fp16 since round 3)
+    assert le == lg, (le, lg)
+    assert ge == gg, (ge, gg)
     # deterministic reductions: a second graphed run reproduces the first bit for bit
     lg2, pg2, _, gg2 = _run(True, name, steps=steps, precision=precision)
     assert lg2 == lg and gg2 == gg, (lg, lg2)
     assert torch.equal(pg2, pg), (pg2 - pg).abs().max().item()
     # eager and graph run the same kernels on the same operands: report how close they are
-    d = (pe - pg).abs().max().item()
-    print(f"eager-vs-graph max |dparam| = {d:.3e}, losses equal: {le == lg}")
-    assert d <= 1e-3 * 0.2, d
+    assert torch.equal(pe, pg), (pe - pg).abs().max().item()
     assert len(set(round(x, 6) for x in lg)) == len(lg), "replays must not repeat masks/losses"
 
 
