@@ -492,10 +492,11 @@ def test_gemm_ext_masked():
 
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("M,N,K", [(4096, 2560, 2560), (1000, 2304, 768), (8192, 768, 3072), (777, 1000, 320),
-                                   (300, 520, 64)])
+                                   (300, 520, 64), (64, 2304, 768), (64, 768, 3072), (7, 3072, 768)])
 def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):
     """Every tile config incl. the split-K ragged-wave tail (triggered for these shapes on 256 CUs)
-    with the full epilogue: bias, LoRA K-ext, gelu, pre-activation, dropout, residual."""
+    and the small-grid split (decode shapes: every tile split into >= 2-k-tile chunks) with the
+    full epilogue: bias, LoRA K-ext, gelu, pre-activation, dropout, residual."""
     C = _C()
     torch.manual_seed(11)
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
@@ -535,3 +536,81 @@ def test_gemm_epilogue_projection_matches_lora_proj(tile, rows, p):
     assert float(t[:, rows if rows > 16 else 16:].abs().max()) == 0.0
     ref_t = ref.dropout(out.float(), p, 4321) @ pw.float().t()
     torch.testing.assert_close(t.float(), ref_t, atol=5e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 7, 64])
+@pytest.mark.parametrize("N,K", [(2304, 768), (768, 3072), (50304, 768), (3072, 768)])
+def test_gemm_skinny_decode_shapes(M, N, K):
+    """M <= 64: the skinny kernel for N <= 4096, K <= 1024 (blocks own 16 columns for all rows, waves
+    split K), the tiled kernels otherwise — the same fused epilogue (bias, LoRA K-ext, gelu,
+    pre-activation, residual) vs the fp32 reference, and equal to the tiled kernel (tile 4) within
+    accumulation-order rounding."""
+    C = _C()
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
+    b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    out, pre = _gnt(C, a, b, bias, a2, b2, 1, None, res, 0.0, 0, True, 1.0, None, 0, None, None, 0.0, 0)
+    exp, exp_pre = ref.gemm_nt(a, b, bias, a2, b2, 1, None, res, 0.0, 0, True)
+    torch.testing.assert_close(pre.float(), exp_pre.float(), atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(out.float(), exp.float(), atol=8e-2, rtol=3e-2)
+    tiled = _gnt(C, a, b, bias, a2, b2, 1, None, res, 0.0, 0, True, 1.0, None, 4, None, None, 0.0, 0)
+    torch.testing.assert_close(out.float(), tiled[0].float(), atol=3e-2, rtol=2e-2)
+    plain = C.gemm_nt(a, b, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0,
+                      None, 32, 0.0, 0)[0]
+    torch.testing.assert_close(plain.float(), a.float() @ b.float().t(), atol=3e-2, rtol=2e-2)
+    again = _gnt(C, a, b, bias, a2, b2, 1, None, res, 0.0, 0, True, 1.0, None, 0, None, None, 0.0, 0)[0]
+    assert torch.equal(out, again)  # deterministic
+
+
+@pytest.mark.parametrize("rows", [8, 24])
+def test_gemm_skinny_epilogue_projection(rows):
+    """The skinny kernel's next-adapter projection slabs == lora_proj over its stored output."""
+    C = _C()
+    torch.manual_seed(9)
+    M, K, N = 64, 768, 3072
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    bias = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    pw = torch.zeros(32, N, device="cuda", dtype=torch.bfloat16)
+    pw[:rows] = (0.05 * torch.randn(rows, N, device="cuda")).to(torch.bfloat16)
+    out, pre, t = C.gemm_nt(a, b, bias, None, None, 1, None, None, 0.0, 0, True, 1.0, None, 0, None, None, 0.0, 0,
+                            pw, rows, 0.0, 4321)
+    exp = C.lora_proj(out, pw, 1.0, 0.0, 4321, rows)
+    torch.testing.assert_close(t.float(), exp.float(), atol=2e-2, rtol=1e-2)
+    assert float(t[:, rows if rows > 16 else 16:].abs().max()) == 0.0
+
+
+def test_decode_tail_matches_torch():
+    """decode_tail == the torch ops it replaces: argmax (first maximal index, ties, -inf rows),
+    pad for finished rows, out[b, col[b]], done |= eos, next ids, col / pos / t advance."""
+    from mift.ops import kernels as K
+    torch.manual_seed(2)
+    B, V, Vp, max_new, fill, pad, eos = 64, 50257, 50304, 16, 7, 50256, 11
+    full = torch.randn(B, Vp, device="cuda").to(torch.bfloat16)
+    full[3, 100] = full[3, 200] = 50.0  # tie: first index wins
+    full[5, :V] = float("-inf")  # all -inf: index 0
+    full[6, 11] = 60.0  # emits eos
+    full[:, V:] = 99.0  # padding columns are never candidates
+    logits = full[:, :V]
+    done = torch.zeros(B, dtype=torch.bool, device="cuda")
+    done[9] = True
+    ids = torch.zeros(B, 1, dtype=torch.long, device="cuda")
+    out = torch.zeros(B, max_new, dtype=torch.long, device="cuda")
+    col = torch.full((B, 1), 4, dtype=torch.long, device="cuda")
+    pos = torch.arange(B, device="cuda")[:, None].clone()
+    t = torch.tensor([33], dtype=torch.int32, device="cuda")
+    d0 = done.clone()
+    K.decode_tail(logits, V, done, ids, out, col, pos, t, fill, pad, eos)
+    nx = logits.float().argmax(-1)
+    assert int(nx[3]) == 100 and int(nx[5]) == 0
+    nx = torch.where(d0, torch.full_like(nx, pad), nx)
+    assert torch.equal(out[:, 4], nx) and int(out[:, :4].abs().sum()) == 0
+    dn = d0 | (nx == eos)
+    assert torch.equal(done, dn) and bool(done[6]) and bool(done[9])
+    assert torch.equal(ids[:, 0], torch.where(dn, torch.full_like(nx, fill), nx))
+    assert int(col.min()) == 5 and int(col.max()) == 5
+    assert torch.equal(pos[:, 0], torch.arange(B, device="cuda") + 1) and int(t) == 34

@@ -111,3 +111,30 @@ def test_lmhead_in_kernel_shift(V, dtype, ignore):
     rl, rg, _ = _ref(h, ln, W, shift_labels(ids, ignore).reshape(-1), V, ignore, gup)
     assert float(loss) == pytest.approx(float(rl), rel=3e-3)
     assert float((hx.grad.float() - rg).norm() / rg.norm()) < 3e-2
+
+
+def test_lmhead_in_launch_total_ignore_and_gmul():
+    """The hygiene folds: the loss total reduced inside the lse launch equals the
+    per-row sum and is bit-stable; the in-kernel ignore id equals masking the labels to -1 first;
+    a gradient multiplier gmul gives the bits of the pre-multiplied fp32 upstream gradient."""
+    V, dtype, ign = 50272, torch.float16, 1
+    h, ln, W, lab, Vp = _case(V, dtype, ign, M=1024)
+    a, _, _ = K.layer_norm_fwd(h, ln.weight, ln.bias, ln.eps)
+    assert mift._ext.require().arrive_ints() == K.ARRIVE_INTS
+    ws = torch.zeros(K.ARRIVE_INTS, dtype=torch.int32, device="cuda")
+    outs = K.lmhead_fwd(a, W, lab, V, 0, ign, ws)
+    E, stats, lse, loss, zlab, total = outs
+    assert total.shape == (1,)
+    assert float(total) == pytest.approx(float(loss.double().sum()), rel=1e-5)
+    assert int(ws.abs().sum()) == 0  # counters reset by the arrivers
+    bits = {tuple(K.lmhead_fwd(a, W, lab, V, 0, ign, ws)[5].view(torch.int32).tolist()) for _ in range(20)}
+    assert len(bits) == 1
+    masked = torch.where(lab == ign, torch.full_like(lab, -1), lab)
+    E2, stats2, lse2, loss2, _ = K.lmhead_fwd(a, W, masked, V)
+    assert torch.equal(loss, loss2) and torch.equal(lse, lse2) and torch.equal(E, E2)
+    Wt = W.t().contiguous()
+    s = torch.tensor([1024.0], device="cuda")
+    m = torch.tensor([1.0 / 4093.0], device="cuda")
+    d1 = K.lmhead_dgrad(E, Wt, W, lab, V, stats, lse, s, 0, ign, m)
+    d2 = K.lmhead_dgrad(E, Wt, W, masked, V, stats, lse, s * m)
+    assert torch.equal(d1, d2)

@@ -21,7 +21,7 @@ for r in range(R):
     row = {}
     for d in ("0", "1", "2", "3"):
         os.environ["MIFT_LM_DBG"] = d
-        row["fused_dbg" + d] = round(t(lambda: C.lmhead_fwd(a, w, lab, V, 0)), 1)
+        row["fused_dbg" + d] = round(t(lambda: C.lmhead_fwd(a, w, lab, V, 0, -1, None)), 1)
     for d in ("0", "1"):
         os.environ["MIFT_LM_DBG"] = d
         row["plain_t8_dbg" + d] = round(t(lambda: C.gemm_nt(a, w, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 8, None, None, 0.0, 0)), 1)
@@ -41,7 +41,7 @@ for nm, x, wt in shapes:
     for g in ("0", "2", "4", "8"):
         os.environ["MIFT_GEMM_GROUP"] = g
         if nm == "lm_head":
-            res["fused_g" + g] = round(t(lambda: C.lmhead_fwd(x, wt, lab, V, 0)), 1)
+            res["fused_g" + g] = round(t(lambda: C.lmhead_fwd(x, wt, lab, V, 0, -1, None)), 1)
         res["plain_g" + g] = round(t(lambda: C.gemm_nt(x, wt, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, 0, None, None, 0.0, 0)), 1)
     os.environ.pop("MIFT_GEMM_GROUP")
     res["torch"] = round(t(lambda: torch.matmul(x, wt.t())), 1)

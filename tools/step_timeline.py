@@ -1,6 +1,6 @@
 """Print the kernel sequence of one training step from a rocprofv3 kernel trace.
 
-  python tools/step_timeline.py <kernel_trace.csv> [delimiter_kernel=adamw_kernel] [which=-2]
+  python tools/step_timeline.py <kernel_trace.csv> [delimiter_kernel=opt_apply_kernel] [which=-2]
 
 Steps are delimited by the optimizer kernel; prints duration, the idle gap
 before each kernel and the workgroup count, then the step's kernel-time sum
@@ -12,7 +12,7 @@ import sys
 
 def main():
     path = sys.argv[1]
-    delim = sys.argv[2] if len(sys.argv) > 2 else "adamw_kernel"
+    delim = sys.argv[2] if len(sys.argv) > 2 else "opt_apply_kernel"
     which = int(sys.argv[3]) if len(sys.argv) > 3 else -2
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))

@@ -191,6 +191,51 @@ MIFT_HD float block_sum(float v, float* scratch) {
   return r;
 }
 
+// In-launch cross-workgroup hand-off ("last block done"), the write-through form of the MI355X
+// guide's Guideline 16: each block stores the values it hands off with mift_st_sc1 (sc1 stores go
+// through the XCD's L2 to memory: no release fence, which would write back the whole L2 from every
+// block — a per-thread __threadfence() here took lmhead_lse from 9 to 139 us and the optimizer stats
+// from 14 to 28 us, profiles/r4/step_timeline_fence_per_thread.txt), waits for them, and calls this.
+// It returns true in every thread of the block that arrives LAST; that block's lane 0 has taken an
+// agent-scope acquire, so plain loads of the handed-off values after it are fresh.  Arrivals are
+// counted in two levels — 8 group counters (block index mod 8), then one top counter taken by
+// each group's last block: same-address agent atomics serialise at the memory side, and 2048
+// blocks on one counter cost lmhead_lse ~24 us (profiles/r4/step_timeline_sc1_one_counter.txt).
+// `counters` = MIFT_ARRIVE_INTS zero-initialised ints (each counter on a 128-B line of its own),
+// reset by the arrivers; launches sharing them must be stream-ordered.
+MIFT_HD void mift_st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+MIFT_HD void mift_st_sc1(float2* p, float2 v) {
+  const unsigned long long bits =
+      (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int MIFT_ARRIVE_INTS = 9 * 32;
+MIFT_HD bool mift_last_block_arrival(unsigned* counters, int* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done
+  __syncthreads();                                    // ... and every other wave's
+  if (threadIdx.x == 0) {
+    const unsigned nb = gridDim.x, g = blockIdx.x & 7u;
+    const unsigned ng = nb < 8u ? nb : 8u, gsize = (nb - g + 7u) >> 3;
+    unsigned* gc = counters + 32 * g;
+    unsigned* top = counters + 32 * 8;
+    int last = 0;
+    if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
+        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = 1;
+      }
+    }
+    *flag_lds = last;
+  }
+  __syncthreads();
+  return *flag_lds != 0;
+}
+
 // 8 packed 16-bit elements -> fp32
 template <typename T>
 MIFT_HD void unpack8(short8 v, float* out) {

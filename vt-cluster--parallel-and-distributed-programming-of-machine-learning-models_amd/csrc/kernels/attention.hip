@@ -18,7 +18,10 @@
 //   Tiles stream through registers: tile t+1's K/V global loads are issued
 //   before tile t's MFMAs (T14 issue-early / write-late).
 //   LDS row strides: every image row is an odd multiple of 32 B, so b128 reads and
-//   transpose reads are bank-conflict free on the same image.
+//   transpose reads are bank-conflict free on the same image; the 16-B staging writes are made
+//   conflict-free by the chunk order of tile_chunk (hd 80's 10-chunk rows would otherwise put a
+//   ds_write_b128 8-lane group across two rows: 2-way, 0.9-1.8 M conflict cycles per dispatch in
+//   round 3's PMC).
 // Backward (FA2 split, no atomics): attn_bwd_dq (mirror of the forward, also
 // computes D = rowsum(dO∘O) for its queries) then attn_bwd_dkdv (one key tile
 // per block, loop over query tiles; S = Q·K^T in the lane-per-key layout,
@@ -94,6 +97,31 @@ MIFT_HD vec8<T> tr_frag(const char* img, int stride, int kbase, int col0, int la
   return f;
 }
 
+// Chunk i of a 64-row tile -> (row r, 16-B chunk c) for the staging copies.  A ds_write_b128
+// serves 8 consecutive lanes per LDS cycle, conflict-free when their 16-B slots (r·stride/16 + c) mod 8
+// are distinct.  Rows of CH % 8 == 0 chunks give every 8-lane group one row.  Head dim 80 (CH = 10)
+// would straddle rows at the b128 image stride 224 B (2-way); there the first 8 chunks of each row go
+// first and chunks 8, 9 of four consecutive rows form the remaining groups — slots (6r + c) mod 8 and
+// (2r + c) mod 8 (b128 / transpose image strides) are then distinct (bank model: 128 -> 0 extra
+// cycles per tile store).  Global loads stay 128-B row segments per 8 lanes.
+template <int HD>
+MIFT_HD void tile_chunk(int i, int& r, int& c) {
+  constexpr int CH = Geo<HD>::CH;
+  if constexpr (CH == 10) {
+    if (i < 64 * 8) {
+      r = i >> 3;
+      c = i & 7;
+    } else {
+      const int j = i - 64 * 8;
+      r = j >> 1;
+      c = 8 + (j & 1);
+    }
+  } else {
+    r = i / CH;
+    c = i % CH;
+  }
+}
+
 // register-staged 64-row tile: global -> regs (issue early) -> LDS image(s) (write late)
 template <int HD>
 struct TileRegs {
@@ -108,7 +136,8 @@ struct TileRegs {
     for (int k = 0; k < G::NCH; ++k) {
       const int i = tid + k * 256;
       if ((64 * G::CH) % 256 == 0 || k + 1 < G::NCH || wv * 64 + k * 256 < 64 * G::CH) {
-        const int r = i / G::CH, c = i % G::CH;
+        int r, c;
+        tile_chunk<HD>(i, r, c);
         const int gr = min(row0 + r, nrows - 1);
         v[k] = *reinterpret_cast<const short8*>(src + (int64_t)gr * ld + c * 8);
       }
@@ -121,7 +150,8 @@ struct TileRegs {
     for (int k = 0; k < G::NCH; ++k) {
       const int i = tid + k * 256;
       if ((64 * G::CH) % 256 == 0 || k + 1 < G::NCH || wv * 64 + k * 256 < 64 * G::CH) {
-        const int r = i / G::CH, c = i % G::CH;
+        int r, c;
+        tile_chunk<HD>(i, r, c);
         *reinterpret_cast<short8*>(img + r * stride + c * 16) = v[k];
       }
     }

@@ -165,3 +165,111 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
 #undef MIFT_DEC
   return out;
 }
+
+namespace {
+
+// ---- greedy decode step tail: ONE launch for what was ~12 small torch kernels per step ----
+// Per row b (one block): next = argmax(logits[b, :V]) — the first index of the maximum, NaN counting
+// as maximal (torch.argmax); a finished row emits pad; out[b, col[b]] = token; done[b] |= token == eos
+// (eos >= 0); the next step's input ids[b] = done ? fill : token; col, pos advance; block 0 advances
+// the cache position t.  16-B logit loads (row stride % 8 == 0), scalar tail.
+MIFT_HD bool argmax_better(float v, int i, float bv, int bi) {
+  const bool vn = v != v, bn = bv != bv;
+  if (vn != bn) return vn;
+  if (vn) return i < bi;
+  return v > bv || (v == bv && i < bi);
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void decode_tail_kernel(const T* __restrict__ logits, int64_t ldl, int V,
+                                                          bool* __restrict__ done, int64_t* __restrict__ ids,
+                                                          int64_t* __restrict__ out, int max_new,
+                                                          int64_t* __restrict__ col, int64_t* __restrict__ pos,
+                                                          int* __restrict__ t, int64_t fill, int64_t pad, int64_t eos) {
+  // 16 waves, each thread's chunks loaded in batches of UN before any compare: the loop was a chain
+  // of dependent loads (27 us per step for 64 x 50257 with one load in flight per thread)
+  constexpr int NTH = 1024, UN = 8;
+  __shared__ float sv[NTH / 64];
+  __shared__ int si[NTH / 64];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const T* row = logits + (int64_t)b * ldl;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  const int nv = V / 8;
+  for (int c0 = tid; c0 < nv; c0 += NTH * UN) {
+    short8 v[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int c = min(c0 + u * NTH, nv - 1);  // clamped: a repeated chunk never wins (same index)
+      v[u] = *reinterpret_cast<const short8*>(row + (int64_t)c * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int c = c0 + u * NTH;
+      if (c >= nv) break;
+      float f[8];
+      unpack8<T>(v[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (argmax_better(f[e], c * 8 + e, best, bi)) { best = f[e]; bi = c * 8 + e; }
+    }
+  }
+  for (int j = nv * 8 + tid; j < V; j += NTH) {
+    const float v = (float)row[j];
+    if (argmax_better(v, j, best, bi)) { best = v; bi = j; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+  }
+  if (lane == 0) { sv[w] = best; si[w] = bi; }
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int k = 1; k < NTH / 64; ++k)
+      if (argmax_better(sv[k], si[k], best, bi)) { best = sv[k]; bi = si[k]; }
+    const bool d0 = done[b];
+    const int64_t tok = d0 ? pad : (int64_t)bi;
+    const int64_t c = col[b];
+    if (c >= 0 && c < max_new) out[(int64_t)b * max_new + c] = tok;
+    const bool d = d0 || (eos >= 0 && tok == eos);
+    done[b] = d;
+    ids[b] = d ? fill : tok;
+    col[b] = c + 1;
+    pos[b] += 1;
+    if (b == 0) t[0] += 1;
+  }
+}
+
+}  // namespace
+
+void mift_decode_tail(const at::Tensor& logits, int64_t V, at::Tensor& done, at::Tensor& ids, at::Tensor& out,
+                      at::Tensor& col, at::Tensor& pos, at::Tensor& t, int64_t fill, int64_t pad, int64_t eos) {
+  const int64_t B = logits.size(0);
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1 && logits.size(1) >= V,
+              "decode_tail: logits [B, >= V], unit column stride");
+  TORCH_CHECK(logits.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0,
+              "decode_tail: 16-B aligned logit rows");
+  TORCH_CHECK(done.scalar_type() == at::kBool && done.numel() == B && done.is_contiguous(), "decode_tail: done [B] bool");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.numel() == B && ids.is_contiguous(), "decode_tail: ids [B] int64");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.dim() == 2 && out.size(0) == B && out.is_contiguous(),
+              "decode_tail: out [B, max_new] int64");
+  TORCH_CHECK(col.scalar_type() == at::kLong && col.numel() == B && col.is_contiguous(), "decode_tail: col [B] int64");
+  TORCH_CHECK(pos.scalar_type() == at::kLong && pos.numel() == B && pos.is_contiguous(), "decode_tail: pos [B] int64");
+  TORCH_CHECK(t.scalar_type() == at::kInt && t.numel() >= 1, "decode_tail: t int32[1]");
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    decode_tail_kernel<T><<<(unsigned)B, 1024, 0, st>>>(
+        reinterpret_cast<const T*>(logits.data_ptr()), logits.stride(0), (int)V, done.data_ptr<bool>(),
+        ids.data_ptr<int64_t>(), out.data_ptr<int64_t>(), (int)out.size(1), col.data_ptr<int64_t>(),
+        pos.data_ptr<int64_t>(), t.data_ptr<int>(), fill, pad, eos);
+  };
+  if (logits.scalar_type() == at::kBFloat16) launch(bf16{});
+  else {
+    TORCH_CHECK(logits.scalar_type() == at::kHalf, "decode_tail: bf16 / fp16 logits");
+    launch(fp16{});
+  }
+}

@@ -77,14 +77,15 @@ struct LmArgs {
   int dbg;                // MIFT_LM_DBG (diagnostics only): bit 0 = skip the E store, bit 2 = no FULL-tile epilogue
   int nt;                 // MIFT_LM_NT (A/B): bit 0 = nontemporal E stores (fwd), bit 1 = nt E loads (dgrad)
   int shift;              // > 0: labels are the UNSHIFTED [B*S] ids, S = shift (see lm_label)
+  int64_t ignore;         // >= 0: this id is no target (OPT ignores its pad id, a real vocabulary entry)
 };
 
 // Target of row `row`: with shift = S the labels tensor holds the unshifted ids and row r's target
 // is ids[r + 1] within its sequence (none for a sequence's last position) — the causal-LM shift done
 // in the kernels instead of by two extra tensor ops per step.
-MIFT_HD int64_t lm_label(const int64_t* labels, int row, int shift) {
-  if (shift <= 0) return labels[row];
-  return (row % shift == shift - 1) ? (int64_t)-1 : labels[row + 1];
+MIFT_HD int64_t lm_label(const int64_t* labels, int row, int shift, int64_t ignore) {
+  const int64_t l = shift <= 0 ? labels[row] : (row % shift == shift - 1) ? (int64_t)-1 : labels[row + 1];
+  return l == ignore ? (int64_t)-1 : l;
 }
 
 struct EpiArgs {
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     // latency hides under the max pass, and no registers held across it (the kernel sits at 256)
     int* labs = reinterpret_cast<int*>(reds + NW * WM);
     if (tid < BM) {
-      const int64_t l = lm_label(lm.labels, min(m0 + tid, M - 1), lm.shift);
+      const int64_t l = lm_label(lm.labels, min(m0 + tid, M - 1), lm.shift, lm.ignore);
       labs[tid] = (l >= 0 && l < V) ? (int)l : -1;
     }
     // Two instantiations of the exp epilogue: every column tile but the last is FULL (no padding
@@ -1087,6 +1088,172 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
                        (const float*)epx.pws, ntn, M, PW, ep.palpha, (T*)ep.pout);
 }
 
+// ---- skinny GEMM (M <= 64 rows: greedy decode, one token per sequence) ----
+// The tiled kernels cover M = 64 with ONE row of 64x64 tiles: 12-48 blocks for the distilgpt2 decode
+// shapes, each running the whole K loop as a chain of dependent tile loads on one CU (8.7 us for
+// 64x2304x768, whose 3.5 MB of weights are 0.45 us of HBM).  Here a block owns BN output columns for
+// all (<= 64) rows and its NW waves take interleaved 32-deep K steps, loading their MFMA fragments
+// straight from global memory (no LDS staging: the 64 activation rows are L2-resident and shared by
+// every block, each weight row is read once) with several k-steps of loads in flight.  The NW partial
+// tiles are summed through LDS in wave order (deterministic), then the gemm_nt epilogue runs on 8-column
+// chunks: bias, LoRA K-extension (one more k-step), pre-add, pre-activation store, forward activation,
+// residual, and the next adapter's input projection as per-column-tile fp32 slabs (proj_reduce_kernel).
+// Not for dropout (training) or activation-backward epilogues: those keep the tiled kernels.
+template <typename T, int BN, int NW>
+__global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                              T* __restrict__ C, const T* __restrict__ A2,
+                                                              const T* __restrict__ B2, int M, int N, int K, int lda,
+                                                              int ldb, int ldc, EpiArgs ep) {
+  constexpr int NT = BN / 16;  // 16-column MFMA tiles per block
+  constexpr int RLD = BN + 4;  // LDS row pitch (floats) of the partial tiles
+  __shared__ __attribute__((aligned(16))) float red[NW][64][RLD];
+  __shared__ __attribute__((aligned(16))) float ot[64][BN + 1];  // rounded output tile (projection)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = blockIdx.x * BN;
+  float4_ acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+  const T* ap[4];
+  const T* bp[NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ap[i] = A + (size_t)min(i * 16 + fr, M - 1) * lda + fq * 8;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) bp[j] = B + (size_t)min(n0 + j * 16 + fr, N - 1) * ldb + fq * 8;
+  const int nks = K / 32;
+  // swapped products (weights first): lane holds out[row i*16 + fr][cols j*16 + 4 fq .. +3]
+#pragma unroll 4
+  for (int ks = w; ks < nks; ks += NW) {
+    const int k = ks * 32;
+    frag_t<T> af[4], bf[NT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const frag_t<T>*>(ap[i] + k);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bf[j] = *reinterpret_cast<const frag_t<T>*>(bp[j] + k);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bf[j], af[i], acc[i][j]);
+  }
+  if (A2 != nullptr && w == NW - 1) {  // LoRA K-extension: one more k-step (the wave with the fewest)
+    frag_t<T> af2[4], bf2[NT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      af2[i] = *reinterpret_cast<const frag_t<T>*>(A2 + (size_t)min(i * 16 + fr, M - 1) * 32 + fq * 8);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      bf2[j] = *reinterpret_cast<const frag_t<T>*>(B2 + (size_t)min(n0 + j * 16 + fr, N - 1) * 32 + fq * 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bf2[j], af2[i], acc[i][j]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      *reinterpret_cast<float4_*>(&red[w][i * 16 + fr][j * 16 + 4 * fq]) = acc[i][j];
+  __syncthreads();
+  const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
+  constexpr int CPR = BN / 8;  // 8-column chunks per row
+  for (int ch = tid; ch < 64 * CPR; ch += NW * 64) {
+    const int row = ch / CPR, c8 = (ch % CPR) * 8;
+    const int gn = n0 + c8;
+    if (row >= M || gn >= N) continue;
+    float z[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = 0.f;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+      const float4 p0 = *reinterpret_cast<const float4*>(&red[v][row][c8]);
+      const float4 p1 = *reinterpret_cast<const float4*>(&red[v][row][c8 + 4]);
+      z[0] += p0.x; z[1] += p0.y; z[2] += p0.z; z[3] += p0.w;
+      z[4] += p1.x; z[5] += p1.y; z[6] += p1.z; z[7] += p1.w;
+    }
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ep.bias != nullptr) {
+      if (ep.bias_f32) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = reinterpret_cast<const float*>(ep.bias)[gn + e];
+      } else {
+        load8<T>(reinterpret_cast<const T*>(ep.bias) + gn, bv);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = (float)(T)(z[e] * alpha + bv[e]);  // the tiled path's 16-bit C tile
+    const size_t off = (size_t)row * ldc + gn;
+    if (ep.pre_add != nullptr) {
+      float pa[8];
+      load8<T>(reinterpret_cast<const T*>(ep.pre_add) + off, pa);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] += pa[e];
+    }
+    if (ep.preact != nullptr) store8<T>(reinterpret_cast<T*>(ep.preact) + off, z);
+    if (ep.act != ACT_NONE) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = apply_act(ep.act, z[e], 0.f);
+    }
+    if (ep.residual != nullptr) {
+      float rv[8];
+      load8<T>(reinterpret_cast<const T*>(ep.residual) + off, rv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] += rv[e];
+    }
+    store8<T>(C + off, z);
+    if (ep.pws != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ot[row][c8 + e] = (float)(T)z[e];
+    }
+  }
+  if (ep.pws == nullptr) return;  // block-uniform
+  // next adapter's input projection over this block's columns: slab[blockIdx][row][j]
+  __syncthreads();
+  const int PW = ep.prow <= 16 ? 16 : 32;
+  float* slab = ep.pws + (size_t)blockIdx.x * M * PW;
+  const T* pw = reinterpret_cast<const T*>(ep.pw);
+  for (int idx = tid; idx < M * PW; idx += NW * 64) {
+    const int r = idx / PW, j = idx % PW;
+    float s = 0.f;
+    if (j < ep.prow) {
+#pragma unroll
+      for (int c = 0; c < BN; ++c) s += ot[r][c] * (float)pw[(size_t)j * N + n0 + c];
+    }
+    slab[(size_t)r * PW + j] = s;
+  }
+}
+
+template <typename T, int BN, int NW>
+void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
+                   int K, const EpiArgs& ep, hipStream_t st) {
+  const int nb = (N + BN - 1) / BN;
+  EpiArgs epx = ep;
+  at::Tensor slab;
+  const int PW = ep.prow <= 16 ? 16 : 32;
+  if (ep.pw != nullptr) {
+    slab = at::empty({(int64_t)nb * M * PW}, a.options().dtype(at::kFloat));
+    epx.pws = slab.data_ptr<float>();
+  }
+  hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW>), dim3(nb), dim3(NW * 64), 0, st, (const T*)a.data_ptr(),
+                     (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0),
+                     (int)c.stride(0), epx);
+  if (ep.pw != nullptr)
+    hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
+                       (const float*)epx.pws, nb, M, PW, ep.palpha, (T*)ep.pout);
+}
+
+// the skinny kernel applies: a forward epilogue without dropout on <= 64 rows (MIFT_GEMM_SKINNY=0: off)
+bool skinny_ok(int M, int N, int K, const EpiArgs& ep) {
+  static const int env = [] { const char* e = getenv("MIFT_GEMM_SKINNY"); return e ? atoi(e) : 1; }();
+  if (!env || M > 64 || N % 16 != 0 || N > 4096 || K > 1024) return false;
+  if (ep.thr != 0 || ep.ext_thr != 0 || ep.aux != nullptr || ep.lm.dbg != 0) return false;
+  if (ep.act != ACT_NONE && ep.act != ACT_GELU_TANH && ep.act != ACT_RELU && ep.act != ACT_GELU_ERF) return false;
+  if (ep.pw != nullptr && ep.pthr != 0) return false;
+  return true;
+}
+
 // Tile configurations (tile id -> geometry):
 //   1: 256x128, 8 waves (4x2), 3-stage ring (144 KiB, 1 block/CU)  — large N
 //   2: 128x64,  4 waves (2x2), 3-stage ring (72 KiB, 2 blocks/CU)  — N ~ 768
@@ -1106,6 +1273,15 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
 template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
+  if (tile == 0 && skinny_ok(M, N, K, ep)) {
+    // decode-sized problems with N <= 4096, K <= 1024: 16-column blocks of 8 waves (48-192 blocks at
+    // the distilgpt2 shapes: c_attn 8.7 -> 5.9 us, c_fc 8.7 -> 6.9).  Every block streams all M x K
+    // activations through its CU, so wide N (the LM head: 32 vs 19.5 us on 128x128 tiles, BN = 32)
+    // and long K (fc2, K = 3072: 16 vs 14 us on the 64x64 split-K path) stay on the tiled kernels
+    // (profiles/r4/decode_skinny_trace.txt).
+    launch_skinny<T, 16, 8>(a, b, c, a2, b2, M, N, K, ep, st);
+    return;
+  }
   if (tile == 0) {
     // auto, from tools/bench_kernels.py on MI355X (profiles/bench_gemm_tiles_sk.json):
     //  * the phased 256x256 kernel (tile 8) wins with >= half a chip-wave of 256x256 tiles at
@@ -1145,26 +1321,50 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
 }
 
 // ---- LM head: loss from the forward's tile statistics (one wave per row) ----
+// Wave w of block b takes rows (b·4 + w) + k·(4·grid), k < rpw.  total != nullptr: also the summed
+// loss — per-block partials (the wave sums in row order, then waves in order), the last block to
+// arrive sums them in block order: deterministic, and no separate reduction launch.  The grid is
+// capped (rpw rows per wave) so few blocks arrive.
 __global__ __launch_bounds__(256) void lmhead_lse_kernel(const float2* __restrict__ stats, int ntn,
                                                          const float* __restrict__ zlab,
                                                          const int64_t* __restrict__ labels, int V, int M, int shift,
-                                                         float* __restrict__ lse, float* __restrict__ loss) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                         int64_t ignore, int rpw, float* __restrict__ lse,
+                                                         float* __restrict__ loss, float* __restrict__ part,
+                                                         unsigned* __restrict__ counter, float* __restrict__ total) {
+  __shared__ float wl[4];
+  __shared__ float red[4];
+  __shared__ int flag;
   const int lane = threadIdx.x & 63;
-  if (row >= M) return;
-  const float2* st = stats + (size_t)row * ntn;
-  float m = -INFINITY;
-  for (int j = lane; j < ntn; j += 64) m = fmaxf(m, st[j].x);
-  m = wave_max(m);
-  float s = 0.f;
-  for (int j = lane; j < ntn; j += 64) s += st[j].y * __expf(st[j].x - m);
-  s = wave_sum(s);
-  if (lane == 0) {
-    const float l = m + __logf(s);
-    lse[row] = l;
-    const int64_t lab = lm_label(labels, row, shift);
-    loss[row] = (lab >= 0 && lab < V) ? l - zlab[row] : 0.f;
+  const int rstride = 4 * gridDim.x;
+  float lsum = 0.f;
+  for (int k = 0; k < rpw; ++k) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6) + k * rstride;
+    if (row >= M) break;  // wave-uniform
+    const float2* st = stats + (size_t)row * ntn;
+    float m = -INFINITY;
+    for (int j = lane; j < ntn; j += 64) m = fmaxf(m, st[j].x);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int j = lane; j < ntn; j += 64) s += st[j].y * __expf(st[j].x - m);
+    s = wave_sum(s);
+    if (lane == 0) {
+      const float l = m + __logf(s);
+      lse[row] = l;
+      const int64_t lab = lm_label(labels, row, shift, ignore);
+      const float lrow = (lab >= 0 && lab < V) ? l - zlab[row] : 0.f;
+      loss[row] = lrow;
+      lsum += lrow;
+    }
   }
+  if (total == nullptr) return;  // block-uniform
+  if (lane == 0) wl[threadIdx.x >> 6] = lsum;
+  __syncthreads();
+  if (threadIdx.x == 0) mift_st_sc1(&part[blockIdx.x], ((wl[0] + wl[1]) + wl[2]) + wl[3]);
+  if (!mift_last_block_arrival(counter, &flag)) return;
+  float t = 0.f;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) t += part[i];
+  t = block_sum<4>(t, red);
+  if (threadIdx.x == 0) total[0] = t;
 }
 
 // ---- LM head: sum the split-K slabs, subtract g·W[label] (the one-hot part of dlogits) ----
@@ -1172,7 +1372,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void lmhead_reduce_kernel(const float* __restrict__ partial, int S, int M, int N,
                                                             const T* __restrict__ w, int ldw,
                                                             const int64_t* __restrict__ labels, int V, int shift,
-                                                            const float* __restrict__ gscale, T* __restrict__ out) {
+                                                            int64_t ignore, const float* __restrict__ gscale,
+                                                            const float* __restrict__ gmul, T* __restrict__ out) {
   const size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;  // one 8-column chunk
   const int cpr = N / 8;
   if (v >= (size_t)M * cpr) return;
@@ -1188,11 +1389,13 @@ __global__ __launch_bounds__(256) void lmhead_reduce_kernel(const float* __restr
     float4 a = p[0], b = p[1];
     acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w; acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
   }
-  const int64_t lab = lm_label(labels, row, shift);
+  const int64_t lab = lm_label(labels, row, shift, ignore);
   if (lab >= 0 && lab < V) {  // dX = g·(softmax·W - W[label]); rows without a target get 0
     float wv[8];
     load8<T>(w + (size_t)lab * ldw + c8, wv);
-    const float g = gscale[0];
+    // g = upstream grad [x gmul: 1/tokens of a replayed step, multiplied here instead of by a
+    // separate scalar kernel; the same fp32 product, so eager and replayed steps agree bitwise]
+    const float g = gmul ? gscale[0] * gmul[0] : gscale[0];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = g * (acc[e] - wv[e]);
   } else {
@@ -1204,7 +1407,7 @@ __global__ __launch_bounds__(256) void lmhead_reduce_kernel(const float* __restr
 
 template <typename T>
 std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int V,
-                                        int shift) {
+                                        int shift, int64_t ignore, const c10::optional<at::Tensor>& ws) {
   const int M = a.size(0), K = a.size(1), N = w.size(0);
   constexpr int BM = 256, BN = 256;
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
@@ -1222,6 +1425,7 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   ep.lm.zlab = zlab.data_ptr<float>();
   ep.lm.ntn = ntn;
   ep.lm.shift = shift;
+  ep.lm.ignore = ignore;
   if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);
   if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   {
@@ -1242,15 +1446,29 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   const int grid = ntm * ntn;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
                      (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
-  hipLaunchKernelGGL(lmhead_lse_kernel, dim3((M + 3) / 4), dim3(256), 0, st,
+  // <= 2 blocks per CU, each wave several rows: few arrivals for the in-launch loss sum
+  const int rows4 = (M + 3) / 4;
+  const int rpw = (rows4 + 2 * num_cus() - 1) / (2 * num_cus());
+  const int lgrid = (rows4 + rpw - 1) / rpw;
+  at::Tensor total, part;
+  if (ws) {
+    total = at::empty({1}, f32);
+    part = at::empty({lgrid}, f32);
+  }
+  hipLaunchKernelGGL(lmhead_lse_kernel, dim3(lgrid), dim3(256), 0, st,
                      reinterpret_cast<const float2*>(stats.data_ptr<float>()), ntn, zlab.data_ptr<float>(),
-                     labels.data_ptr<int64_t>(), V, M, shift, lse.data_ptr<float>(), loss.data_ptr<float>());
+                     labels.data_ptr<int64_t>(), V, M, shift, ignore, rpw, lse.data_ptr<float>(), loss.data_ptr<float>(),
+                     ws ? part.data_ptr<float>() : nullptr,
+                     ws ? reinterpret_cast<unsigned*>(ws->data_ptr<int>()) : nullptr,
+                     ws ? total.data_ptr<float>() : nullptr);
+  if (ws) return {E, stats, lse, loss, zlab, total};
   return {E, stats, lse, loss, zlab};
 }
 
 template <typename T>
 at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
-                             int V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale, int shift) {
+                             int V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale, int shift,
+                             int64_t ignore, const c10::optional<at::Tensor>& gmul) {
   const int M = E.size(0), K = E.size(1), N = wt.size(0);
   const int ntn_f = stats.size(1);
   constexpr int BM = 256, BN = 256;
@@ -1276,6 +1494,7 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   ep.lm.gpc = gpc;
   ep.lm.partial = partial.data_ptr<float>();
   ep.lm.shift = shift;
+  ep.lm.ignore = ignore;
   if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   SkArgs sk{};
   auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
@@ -1291,7 +1510,8 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   const size_t chunks = (size_t)M * (N / 8);
   hipLaunchKernelGGL(lmhead_reduce_kernel<T>, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st,
                      partial.data_ptr<float>(), S, M, N, (const T*)w.data_ptr(), (int)w.stride(0),
-                     labels.data_ptr<int64_t>(), V, shift, gscale.data_ptr<float>(), (T*)out.data_ptr());
+                     labels.data_ptr<int64_t>(), V, shift, ignore, gscale.data_ptr<float>(),
+                     gmul ? gmul->data_ptr<float>() : nullptr, (T*)out.data_ptr());
   return out;
 }
 
@@ -1300,9 +1520,11 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
 // Fused LM head + cross-entropy forward: a = LN(h) [M,K], w = tied embedding [V_pad,K],
 // labels [M] int64 (ignore -> any value outside [0, V)): the targets themselves (shift = 0), or the
 // unshifted ids of sequences of length shift (row r's target = ids[r + 1] inside its sequence).
-// -> (E [M,V_pad] = exp(z - m_tile) 16-bit, stats [M, V_pad/256, 2] (m, s), lse [M], loss [M], zlab [M]).
+// -> (E [M,V_pad] = exp(z - m_tile) 16-bit, stats [M, V_pad/256, 2] (m, s), lse [M], loss [M], zlab [M]
+//     [, total [1] = Σ loss, when `ws` (an int32 zero-initialised arrival counter) is given]).
+// ignore >= 0: that id is no target.
 std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V,
-                                        int64_t shift) {
+                                        int64_t shift, int64_t ignore, const c10::optional<at::Tensor>& ws) {
   TORCH_CHECK(a.is_cuda() && w.is_cuda() && labels.is_cuda(), "lmhead_fwd: GPU tensors");
   TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1), "lmhead_fwd: a [M,K], w [V_pad,K]");
   TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && a.size(1) % 64 == 0, "lmhead_fwd: K-contiguous, K % 64 == 0");
@@ -1312,17 +1534,20 @@ std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w
               "lmhead_fwd: int64 labels [M]");
   TORCH_CHECK(shift >= 0 && (shift == 0 || a.size(0) % shift == 0), "lmhead_fwd: rows must be whole sequences");
   TORCH_CHECK(a.scalar_type() == w.scalar_type(), "lmhead_fwd: dtype mismatch");
-  if (a.scalar_type() == at::kBFloat16) return lmhead_fwd_impl<bf16>(a, w, labels, (int)V, (int)shift);
+  TORCH_CHECK(!ws || (ws->is_cuda() && ws->scalar_type() == at::kInt && ws->numel() >= MIFT_ARRIVE_INTS),
+              "lmhead_fwd: ws int32[arrive_ints]");
+  if (a.scalar_type() == at::kBFloat16) return lmhead_fwd_impl<bf16>(a, w, labels, (int)V, (int)shift, ignore, ws);
   TORCH_CHECK(a.scalar_type() == at::kHalf, "lmhead_fwd: bf16/fp16");
-  return lmhead_fwd_impl<fp16>(a, w, labels, (int)V, (int)shift);
+  return lmhead_fwd_impl<fp16>(a, w, labels, (int)V, (int)shift, ignore, ws);
 }
 
 // Backward of the fused head: dX [M,N] = g·(softmax - onehot)·W without materialising dlogits.
 // E / stats / lse from mift_lmhead_fwd; wt = Wᵀ [N, V_pad] (K-contiguous), w = W [V_pad, N];
-// gscale: 1-element fp32 device tensor (upstream gradient, e.g. loss_scale / tokens).
+// gscale: 1-element fp32 device tensor (upstream gradient, e.g. loss_scale / tokens), times the
+// optional 1-element fp32 gmul.
 at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
                              int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale,
-                             int64_t shift) {
+                             int64_t shift, int64_t ignore, const c10::optional<at::Tensor>& gmul) {
   TORCH_CHECK(E.is_cuda() && wt.is_cuda() && w.is_cuda(), "lmhead_dgrad: GPU tensors");
   TORCH_CHECK(E.dim() == 2 && wt.dim() == 2 && wt.size(1) == E.size(1), "lmhead_dgrad: E [M,V_pad], wt [N,V_pad]");
   TORCH_CHECK(E.stride(1) == 1 && wt.stride(1) == 1 && E.size(1) % 64 == 0, "lmhead_dgrad: V_pad % 64 == 0");
@@ -1336,9 +1561,12 @@ at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at
   TORCH_CHECK(lse.numel() == E.size(0) && gscale.numel() >= 1 && gscale.scalar_type() == at::kFloat,
               "lmhead_dgrad: lse [M], fp32 gscale");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == E.size(0), "lmhead_dgrad: labels");
-  if (E.scalar_type() == at::kBFloat16) return lmhead_dgrad_impl<bf16>(E, wt, w, labels, (int)V, stats, lse, gscale, (int)shift);
+  TORCH_CHECK(!gmul || (gmul->is_cuda() && gmul->scalar_type() == at::kFloat && gmul->numel() >= 1),
+              "lmhead_dgrad: gmul fp32[1]");
+  if (E.scalar_type() == at::kBFloat16)
+    return lmhead_dgrad_impl<bf16>(E, wt, w, labels, (int)V, stats, lse, gscale, (int)shift, ignore, gmul);
   TORCH_CHECK(E.scalar_type() == at::kHalf, "lmhead_dgrad: bf16/fp16");
-  return lmhead_dgrad_impl<fp16>(E, wt, w, labels, (int)V, stats, lse, gscale, (int)shift);
+  return lmhead_dgrad_impl<fp16>(E, wt, w, labels, (int)V, stats, lse, gscale, (int)shift, ignore, gmul);
 }
 
 // out = epi(a @ b^T [+ a2 @ b2^T]).  a:[M,K], b:[N,K] (K-contiguous, K%64==0).

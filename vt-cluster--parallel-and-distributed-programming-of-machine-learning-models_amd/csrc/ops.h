@@ -28,10 +28,10 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
 
 // ---- K2/K7 fused LM head + cross-entropy (kernels/gemm.hip, EPI 1/2)
 std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V,
-                                        int64_t shift);
+                                        int64_t shift, int64_t ignore, const c10::optional<at::Tensor>& ws);
 at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
                              int64_t V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale,
-                             int64_t shift);
+                             int64_t shift, int64_t ignore, const c10::optional<at::Tensor>& gmul);
 
 // ---- LoRA side path (kernels/lora.hip)
 at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed,
@@ -67,6 +67,13 @@ std::vector<at::Tensor> mift_xent_fwd_bwd(at::Tensor& logits, const at::Tensor& 
 void mift_grad_stats(const at::Tensor& g, at::Tensor& stats);
 void mift_opt_finalize(const at::Tensor& stats, at::Tensor& state, double max_norm, bool dynamic_scale,
                        double growth_factor, double backoff_factor, int64_t growth_interval);
+void mift_opt_stats(const at::Tensor& g, at::Tensor& stats, at::Tensor& ws, at::Tensor& state, bool finalize,
+                    double max_norm, bool dynamic_scale, double growth_factor, double backoff_factor,
+                    int64_t growth_interval);
+void mift_opt_apply(at::Tensor& p, at::Tensor& g, at::Tensor& m, at::Tensor& v, double lr, at::Tensor& state,
+                    const at::Tensor& stats, at::Tensor& ws, bool finalize, double max_norm, bool dynamic_scale,
+                    double growth_factor, double backoff_factor, int64_t growth_interval, double beta1, double beta2,
+                    double eps, double wd);
 void mift_adamw(at::Tensor& p, at::Tensor& g, at::Tensor& m, at::Tensor& v, const at::Tensor& lr_t,
                 const at::Tensor& state, double beta1, double beta2, double eps, double wd);
 
@@ -84,11 +91,14 @@ at::Tensor mift_attn_bwd_bits(const at::Tensor& dout, const at::Tensor& qkv, con
                               const c10::optional<at::Tensor>& kv_len, const c10::optional<at::Tensor>& bits);
 
 // ---- K12 decode attention over a KV cache (kernels/decode.hip)
+void mift_decode_tail(const at::Tensor& logits, int64_t V, at::Tensor& done, at::Tensor& ids, at::Tensor& out,
+                      at::Tensor& col, at::Tensor& pos, at::Tensor& t, int64_t fill, int64_t pad, int64_t eos);
 at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
                             const c10::optional<at::Tensor>& start, const c10::optional<at::Tensor>& plen,
                             int64_t gend, const c10::optional<at::Tensor>& t_dev);
 
 #define MIFT_BIND_MORE(m) \
+  m.def("decode_tail", &mift_decode_tail, "greedy decode step tail: argmax, pad/eos, next ids, out/col/pos/t advance"); \
   m.def("decode_attn", &mift_decode_attn, "single-token attention over a KV cache; appends k/v at t (left padding: start; prompt gap: plen, gend)"); \
   m.def("lora_proj", &mift_lora_proj, "out[M,32] = alpha*drop(x)@w^T (tall-skinny MFMA)"); \
   m.def("layer_norm_fwd_proj", &mift_layer_norm_fwd_proj, "LN fwd + alpha*drop(y)@pw^T -> (y, mean, rstd, proj)"); \
@@ -107,11 +117,14 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
         pybind11::arg("tile"), pybind11::arg("alpha_t"), pybind11::arg("pre_add"), pybind11::arg("ext_p"), \
         pybind11::arg("ext_seed"), pybind11::arg("proj_w") = pybind11::none(), pybind11::arg("proj_rows") = 32, \
         pybind11::arg("proj_p") = 0.0, pybind11::arg("proj_seed") = 0); \
-  m.def("lmhead_fwd", &mift_lmhead_fwd, "fused LM head + CE fwd -> (E, stats, lse, loss, zlab)"); \
+  m.def("lmhead_fwd", &mift_lmhead_fwd, "fused LM head + CE fwd -> (E, stats, lse, loss, zlab[, total])"); \
   m.def("lmhead_dgrad", &mift_lmhead_dgrad, "fused LM head + CE dgrad -> dX (no dlogits)"); \
   m.def("grad_stats", &mift_grad_stats, "sum(g^2), nonfinite count -> stats[2]"); \
   m.def("opt_finalize", &mift_opt_finalize, "clip coef / found_inf / step / loss-scale update"); \
   m.def("adamw", &mift_adamw, "fused AdamW over a flat fp32 arena (zeroes grads)"); \
+  m.def("opt_stats", &mift_opt_stats, "grad stats + in-launch fixed-order reduce [+ finalize]"); \
+  m.def("arrive_ints", []() { return (int64_t)MIFT_ARRIVE_INTS; }, "int32 words of an in-launch arrival-counter set"); \
+  m.def("opt_apply", &mift_opt_apply, "AdamW [+ finalize from all-reduced stats] (zeroes grads)"); \
   m.def("mask_scale", &mift_mask_scale, "counter-hash dropout (fwd == bwd), optional accumulate"); \
   m.def("act_bwd", &mift_act_bwd, "dz = dropmask(g) * act'(z)"); \
   m.def("embed_fwd", &mift_embed_fwd, "token + position gather (+dropout)"); \

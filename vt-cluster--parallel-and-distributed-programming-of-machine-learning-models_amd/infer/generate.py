@@ -133,6 +133,7 @@ class _DecodeGraph:
         self.cache = KVCache(L, B, H, S0 + max_new, hd, dtype, dev)
         self.B, self.S0, self.H, self.hd, self.fill, self.pad, self.eos = B, S0, H, hd, fill, pad, eos
         self.nxt = torch.zeros(B, dtype=torch.long, device=dev)
+        self.ids = torch.zeros(B, 1, dtype=torch.long, device=dev)  # this step's input token per row
         self.done = torch.zeros(B, dtype=torch.bool, device=dev)
         self.t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.pos = torch.zeros(B, 1, dtype=torch.long, device=dev)
@@ -142,21 +143,18 @@ class _DecodeGraph:
         self.graph = None
 
     def step(self, model):
-        """One decode step on the static state (eager, or recorded during capture)."""
+        """One decode step on the static state (eager, or recorded during capture).  The greedy tail —
+        argmax, pad for finished rows, the output column, EOS flags, the next input ids and the
+        position / column / cache-position advance — is ONE kernel (``decode_tail``; it was ~12 torch
+        kernels per step)."""
+        from ..ops import kernels as K
         B, H, hd = self.B, self.H, self.hd
-        ids = torch.where(self.done, torch.full_like(self.nxt, self.fill), self.nxt)[:, None]
-        h = model.embed_at(ids, self.pos)
+        h = model.embed_at(self.ids, self.pos)
         h = _run_blocks(model, h, lambda li: _decode_attn(self.cache, li, B, H, hd, self.t, self.plen, self.S0, True),
                         True)
-        nx = model.head_logits(h)[:, -1].float().argmax(-1)
-        nx = torch.where(self.done, torch.full_like(nx, self.pad), nx)
-        self.out.scatter_(1, self.col, nx[:, None])
-        if self.eos is not None:
-            self.done |= nx == self.eos
-        self.nxt.copy_(nx)
-        self.t += 1
-        self.pos += 1
-        self.col += 1
+        logits = model.head_logits(h)[:, -1]
+        K.decode_tail(logits, logits.shape[-1], self.done, self.ids, self.out, self.col, self.pos, self.t, self.fill,
+                      self.pad, self.eos)
 
     def run(self, model, nsteps):
         if nsteps <= 0:
@@ -275,6 +273,7 @@ def _graphed_decode(dg, model, input_ids, nxt, lens, max_new_tokens, pad, eos):
     done = torch.zeros_like(dg.done) if eos is None else (nxt == eos)
     dg.nxt.copy_(nxt)
     dg.done.copy_(done)
+    dg.ids.copy_(torch.where(done, torch.full_like(nxt, dg.fill), nxt)[:, None])
     dg.out.zero_()
     dg.out[:, 0] = nxt
     dg.t.fill_(dg.S0)

@@ -496,22 +496,30 @@ class LMHeadXent(torch.autograd.Function):
     ``Cluster/Project 2 - Course Project/finetune_lora_opt_pp.py:138-153``.
 
     ``MIFT_LMHEAD=blas`` selects the previous library path (hipBLASLt logits + xent kernel +
-    hipBLASLt dgrad) for A/B measurements."""
+    hipBLASLt dgrad) for A/B measurements.
+
+    No torch kernels around the two launches: the ignored id (OPT's pad) is masked inside the
+    kernels, the loss sum comes out of ``lmhead_lse_kernel`` (deterministic in-launch reduction,
+    ``_lm_ws``), and a replayed step's 1/tokens factor (``head_grad_mul``) is multiplied into the
+    upstream gradient inside the dgrad reduction — VERDICT r3 hygiene (the per-step fill / binary /
+    reduce / copy kernels of the graph)."""
 
     @staticmethod
     def forward(ctx, h, ln_w, ln_b, eps, w_nk, labels, V, ignore_index, need_grad, w_kn, shift):
         shp = h.shape
         h2 = _flat(h.contiguous())
         a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
-        lab = labels.reshape(-1)
-        if ignore_index >= 0:  # e.g. OPT ignores the pad id, a real vocabulary entry
-            lab = torch.where(lab == ignore_index, torch.full_like(lab, -1), lab)
-        lab = lab.contiguous()
-        E, stats, lse, loss_rows, _ = K.lmhead_fwd(a, w_nk, lab, V, shift)
+        lab = labels.reshape(-1).contiguous()
+        ign = int(ignore_index) if ignore_index >= 0 else -1  # e.g. OPT ignores the pad id, a real entry
+        outs = K.lmhead_fwd(a, w_nk, lab, V, shift, ign, _lm_ws(a.device))
+        E, stats, lse, total = outs[0], outs[1], outs[2], outs[5]
         if need_grad:
             ctx.save_for_backward(h2, mean, rstd, ln_w, E, stats, lse, lab)
-        ctx.shp, ctx.w_nk, ctx.w_kn, ctx.V, ctx.shift = shp, w_nk, w_kn, V, shift
-        return loss_rows.sum()
+        ctx.shp, ctx.w_nk, ctx.w_kn, ctx.V, ctx.shift, ctx.ign = shp, w_nk, w_kn, V, shift, ign
+        ctx.gmul = _HEAD_GMUL[0]
+        if ctx.gmul is not None:
+            _HEAD_GMUL[1] = True
+        return total.view(())
 
     @staticmethod
     def backward(ctx, g):
@@ -519,7 +527,7 @@ class LMHeadXent(torch.autograd.Function):
         w_kn = ctx.w_kn if ctx.w_kn is not None else ctx.w_nk.t().contiguous()
         g1 = g.reshape(1)
         da = K.lmhead_dgrad(E, w_kn, ctx.w_nk, lab, ctx.V, stats, lse, g1 if g1.dtype == torch.float32 else g1.float(),
-                            ctx.shift)
+                            ctx.shift, ctx.ign, ctx.gmul)
         dh, _, _, _ = K.layer_norm_bwd(da, h2, ln_w, mean, rstd)
         return dh.view(ctx.shp), None, None, None, None, None, None, None, None, None, None
 
@@ -558,6 +566,32 @@ class LMHeadXentBlas(torch.autograd.Function):
         da = (da.float() * g.reshape(1).float()).to(dlogits.dtype)  # upstream grad applied in fp32
         dh, _, _, _ = K.layer_norm_bwd(da, h2, ln_w, mean, rstd)
         return dh.view(ctx.shp), None, None, None, None, None, None, None, None
+
+
+_LM_WS = {}
+_HEAD_GMUL = [None, False]  # (multiplier tensor, consumed by a head since set_head_grad_mul)
+
+
+def _lm_ws(dev):
+    """Per-device zero-initialised arrival counter of the LM head's in-launch loss reduction
+    (self-resetting; the head's launches on a device are stream-ordered).  Created by the first
+    (eager, warm-up) call, never inside a graph capture."""
+    ws = _LM_WS.get(dev)
+    if ws is None:
+        ws = _LM_WS[dev] = torch.zeros(K.ARRIVE_INTS, dtype=torch.int32, device=dev)
+    return ws
+
+
+def set_head_grad_mul(t):
+    """Make the next fused LM heads multiply their upstream gradient by the fp32 device scalar ``t``
+    (None: off).  The graph-captured step passes its per-step 1/tokens here and seeds backward with
+    the bare loss scale; ``head_grad_mul_used()`` tells whether a head took it (else the caller
+    must scale the seed itself)."""
+    _HEAD_GMUL[0], _HEAD_GMUL[1] = t, False
+
+
+def head_grad_mul_used():
+    return _HEAD_GMUL[1]
 
 
 def _xent_chunk(M, Vp):

@@ -81,19 +81,35 @@ def pack_lora(A, B, a_scale, dtype):
     return C().pack_lora(A, B, float(a_scale), dtype)
 
 
-def lmhead_fwd(a, w_nk, labels, V, shift=0):
-    """Fused LM head + CE forward -> (E, stats, lse, loss_rows, zlab); labels outside [0, V) ignored.
-    ``shift = S``: labels are the unshifted ids of length-S sequences (row r's target is ids[r + 1])."""
-    return C().lmhead_fwd(a, w_nk, labels, int(V), int(shift))
+# int32 words of one in-launch arrival-counter set (csrc/common.h MIFT_ARRIVE_INTS: 8 group counters
+# + 1 top counter, one 128-B line each); the kernels check the size they are given
+ARRIVE_INTS = 9 * 32
 
 
-def lmhead_dgrad(E, w_kn, w_nk, labels, V, stats, lse, gscale, shift=0):
-    """dX = g·(softmax - onehot)·W from the forward's E / tile stats (no dlogits)."""
-    return C().lmhead_dgrad(E, w_kn, w_nk, labels, int(V), stats, lse, gscale, int(shift))
+def lmhead_fwd(a, w_nk, labels, V, shift=0, ignore_index=-1, ws=None):
+    """Fused LM head + CE forward -> (E, stats, lse, loss_rows, zlab[, total]); labels outside [0, V)
+    and ``ignore_index`` (>= 0) are no target.  ``shift = S``: labels are the unshifted ids of length-S
+    sequences (row r's target is ids[r + 1]).  ``ws`` (int32[ARRIVE_INTS], zero, stream-ordered users): the
+    kernel also returns the summed loss ``total`` [1] (deterministic in-launch reduction)."""
+    return C().lmhead_fwd(a, w_nk, labels, int(V), int(shift), int(ignore_index), ws)
+
+
+def lmhead_dgrad(E, w_kn, w_nk, labels, V, stats, lse, gscale, shift=0, ignore_index=-1, gmul=None):
+    """dX = g·(softmax - onehot)·W from the forward's E / tile stats (no dlogits); g = gscale[0]
+    (x gmul[0] when given)."""
+    return C().lmhead_dgrad(E, w_kn, w_nk, labels, int(V), stats, lse, gscale, int(shift), int(ignore_index), gmul)
 
 
 def xent(logits, labels, V, ignore_index=-100, write_grad=True):
     return C().xent_fwd_bwd(logits, labels, int(V), int(ignore_index), bool(write_grad))
+
+
+def decode_tail(logits, V, done, ids, out, col, pos, t, fill, pad, eos):
+    """One launch per greedy decode step (csrc/kernels/decode.hip): token = argmax(logits[b, :V])
+    (first maximal index), ``pad`` for finished rows, out[b, col[b]] = token, done |= token == eos
+    (eos None: never), ids[b] = done ? fill : token, col / pos / t += 1 — all in place."""
+    C().decode_tail(logits, int(V), done, ids, out, col, pos, t, int(fill), int(pad),
+                    -1 if eos is None else int(eos))
 
 
 def decode_attn(qkv, kcache, vcache, t, scale, start=None, plen=None, gend=0):

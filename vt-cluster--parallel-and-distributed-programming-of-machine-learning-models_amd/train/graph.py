@@ -68,24 +68,37 @@ class GraphedStep:
 
     # ------------------------------------------------------------------
     def _fwd_bwd(self, ent, n):
-        """The captured region: forward + backward of every micro-batch."""
+        """The captured region: forward + backward of every micro-batch.  Returns the step's summed
+        loss — a tensor of the graph's pool that every replay rewrites (no copy kernel)."""
         tr, model = self.tr, self.tr.model
         C = _C()
-        # the scaled upstream gradient seeds backward directly (no ones-fill + multiply kernels)
-        gscale = (tr.opt.loss_scale_t * ent["inv_ntok"]).reshape(())
+        from ..ops import fused
+        gscale = None
+        acc = None
         for i in range(n):
             C.set_seed_step(ent["steps_t"][i:i + 1])
             mb = ent["static"][i]
-            out = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"], labels=mb["labels"],
-                        reduction="sum", return_logits=False)
+            # the fused LM head multiplies its upstream grad by 1/tokens inside its dgrad reduction,
+            # so backward is seeded with the loss scale itself: no scalar multiply kernel per step
+            fused.set_head_grad_mul(ent["inv_ntok"])
+            try:
+                out = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"], labels=mb["labels"],
+                            reduction="sum", return_logits=False)
+                used = fused.head_grad_mul_used()
+            finally:
+                fused.set_head_grad_mul(None)
             loss_sum = out["loss"].float()
-            loss_sum.backward(gscale)
+            if used:
+                seed = tr.opt.loss_scale_t.reshape(())
+            else:  # a head without the multiplier (library / classification heads)
+                if gscale is None:
+                    gscale = (tr.opt.loss_scale_t * ent["inv_ntok"]).reshape(())
+                seed = gscale
+            loss_sum.backward(seed)
             streams.join()
-            if i == 0:
-                ent["loss"].copy_(loss_sum.detach())
-            else:
-                ent["loss"].add_(loss_sum.detach())
+            acc = loss_sum.detach() if acc is None else acc + loss_sum.detach()
         C.set_seed_step(None)
+        return acc
 
     # Per-step inputs of a replay — every micro-batch tensor, the micro-step counters and 1/tokens —
     # live in ONE device buffer that one async copy refreshes from a ring of pinned staging buffers
@@ -113,7 +126,7 @@ class GraphedStep:
         for i, k, off, n, dt, shp in items:
             static[i][k] = dbuf[off:off + n].view(dt).view(shp)
         pin = torch.cuda.is_available()
-        ent = {"static": static, "loss": torch.zeros((), dtype=torch.float32, device=dev),
+        ent = {"static": static, "loss": None,
                "steps_t": dbuf[steps_off:steps_off + 8 * len(mbs)].view(torch.int64),
                "inv_ntok": dbuf[inv_off:inv_off + 4].view(torch.float32),
                "dbuf": dbuf, "items": items, "steps_off": steps_off, "inv_off": inv_off,
@@ -140,7 +153,7 @@ class GraphedStep:
             # collectives are never captured: the DP buckets launch after the replay (finish())
             with (red.no_sync() if red is not None else _nullctx()):
                 with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
-                    self._fwd_bwd(ent, len(mbs))
+                    ent["loss"] = self._fwd_bwd(ent, len(mbs))
         finally:
             if gc_was:
                 gc.enable()

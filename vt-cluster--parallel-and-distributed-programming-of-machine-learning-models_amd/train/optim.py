@@ -1,7 +1,9 @@
 """Fused AdamW + global-norm clip + dynamic loss scaling over a flat arena.
 
 One object drives both execution paths with identical semantics:
-  * GPU: three HIP launches (csrc/kernels/adamw.hip), no host sync;
+  * GPU: two HIP launches (csrc/kernels/adamw.hip ``opt_stats`` + ``opt_apply``), no host sync and
+    no per-step device fill: the learning rate is a launch argument, the clip / found-inf / loss-scale
+    finalize runs inside one of the two launches (after the stats all-reduce when there is one);
   * CPU: the same math in torch ops (reference / world_size=1 plumbing).
 
 State tensor layout (device, fp32): [step, loss_scale, good_steps,
@@ -34,11 +36,14 @@ class FusedAdamW:
         self.max_grad_norm = max_grad_norm
         self.dynamic = loss_scale == "dynamic"
         dev = params.device
-        self.lr_t = torch.tensor([lr], dtype=torch.float32, device=dev)
+        self.lr = float(lr)
         self.base_lr = lr
         scale = init_scale if self.dynamic else 1.0
         self.state = torch.tensor([0.0, scale, 0.0, 1.0, 0.0, 0.0], dtype=torch.float32, device=dev)
         self.stats_buf = torch.zeros(2, dtype=torch.float32, device=dev)
+        from ..ops.kernels import ARRIVE_INTS
+        # the kernels' self-resetting arrival counters: opt_stats' set, then opt_apply's counter
+        self.ws = torch.zeros(ARRIVE_INTS + 32, dtype=torch.int32, device=dev)
         self.growth_interval = growth_interval
         # sum(g^2) / non-finite count are summed over every group holding a disjoint part
         # of the parameters (pipeline stages, ZeRO-1 shards)
@@ -52,26 +57,28 @@ class FusedAdamW:
         return self.state[1:2]
 
     def set_lr(self, lr: float):
-        self.lr_t.fill_(lr)
+        self.lr = float(lr)
 
     def step(self):
+        reduce = dist.is_initialized() and bool(self.groups)
         if self.kernels:
             K = C()
-            K.grad_stats(self.g, self.stats_buf)
-        else:
-            self.stats_buf[0] = (self.g * self.g).sum()
-            self.stats_buf[1] = (~torch.isfinite(self.g)).sum().float()
-        if dist.is_initialized():
+            fin = (float(self.max_grad_norm or 0.0), self.dynamic, 2.0, 0.5, self.growth_interval)
+            # no all-reduce of the stats: finalize inside opt_stats; else inside opt_apply
+            K.opt_stats(self.g, self.stats_buf, self.ws, self.state, not reduce, *fin)
+            if reduce:
+                for grp in self.groups:
+                    dist.all_reduce(self.stats_buf, group=grp)
+            K.opt_apply(self.p, self.g, self.m, self.v, self.lr, self.state, self.stats_buf, self.ws, reduce, *fin,
+                        self.betas[0], self.betas[1], self.eps, self.wd)
+            return
+        self.stats_buf[0] = (self.g * self.g).sum()
+        self.stats_buf[1] = (~torch.isfinite(self.g)).sum().float()
+        if reduce:
             for grp in self.groups:
                 dist.all_reduce(self.stats_buf, group=grp)
-        if self.kernels:
-            K.opt_finalize(self.stats_buf, self.state, float(self.max_grad_norm or 0.0), self.dynamic, 2.0, 0.5,
-                           self.growth_interval)
-            K.adamw(self.p, self.g, self.m, self.v, self.lr_t, self.state, self.betas[0], self.betas[1], self.eps,
-                    self.wd)
-        else:
-            self._finalize_ref()
-            self._adamw_ref()
+        self._finalize_ref()
+        self._adamw_ref()
 
     def _finalize_ref(self):
         s = self.state
@@ -102,7 +109,7 @@ class FusedAdamW:
             return
         b1, b2 = self.betas
         step = s[0].item()
-        lr = self.lr_t.item()
+        lr = torch.tensor(self.lr, dtype=torch.float32).item()  # fp32 lr, as the kernel sees it
         g = self.g * s[3]
         self.m.mul_(b1).add_(g, alpha=1 - b1)
         self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
@@ -119,13 +126,14 @@ class FusedAdamW:
         return {"step": int(s[0]), "loss_scale": s[1], "grad_norm": s[5], "found_inf": bool(s[4])}
 
     def state_dict(self):
-        return {"m": self.m.cpu(), "v": self.v.cpu(), "state": self.state.cpu(), "lr": self.lr_t.cpu()}
+        return {"m": self.m.cpu(), "v": self.v.cpu(), "state": self.state.cpu(),
+                "lr": torch.tensor([self.lr], dtype=torch.float32)}
 
     def load_state_dict(self, sd):
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
         self.state.copy_(sd["state"])
-        self.lr_t.copy_(sd["lr"])
+        self.lr = float(sd["lr"].reshape(-1)[0])
 
 
 def linear_schedule(base_lr: float, total_steps: int, warmup: int = 0):
