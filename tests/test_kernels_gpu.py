@@ -313,6 +313,8 @@ def test_lora_proj_and_wgrad(p, K, M, nz):
     out = C.lora_proj(x, w, 2.0, p, 55, nz)
     xd = ref.dropout(x.float(), p, 55)
     torch.testing.assert_close(out.float(), 2.0 * xd @ w.float().t(), atol=3e-2, rtol=3e-2)
+    # K-split shapes reduce in the launch (per-row-block arrival counters, re-armed): same bits again
+    assert torch.equal(C.lora_proj(x, w, 2.0, p, 55, nz), out)
     if M > 4096:
         return
     y = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
@@ -614,3 +616,25 @@ def test_decode_tail_matches_torch():
     assert torch.equal(ids[:, 0], torch.where(dn, torch.full_like(nx, fill), nx))
     assert int(col.min()) == 5 and int(col.max()) == 5
     assert torch.equal(pos[:, 0], torch.arange(B, device="cuda") + 1) and int(t) == 34
+
+
+@pytest.mark.parametrize("M", [1, 13, 64])
+@pytest.mark.parametrize("N,K,act", [(2304, 768, 0), (3072, 768, 1), (1024, 1024, 2)])
+def test_gemm_ln_prologue(M, N, K, act):
+    """gemm_ln (decode): act(LayerNorm(x) @ w.T + bias) in one launch == layer_norm_fwd + gemm_nt."""
+    from mift.ops import kernels as K_
+    torch.manual_seed(4)
+    x = (torch.randn(M, K, device="cuda") * 3 + 1).to(torch.bfloat16)
+    lw = (1 + 0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    lb = (0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    bias = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    assert K_.gemm_ln_ok(x, w, lw)
+    y = K_.gemm_ln(x, lw, lb, 1e-5, w, bias, act=act)
+    a, _, _ = K_.layer_norm_fwd(x, lw, lb, 1e-5)
+    exp = K_.gemm(a, w, bias, act=act, tile=4)
+    torch.testing.assert_close(y.float(), exp.float(), atol=3e-2, rtol=2e-2)
+    ref_a = torch.nn.functional.layer_norm(x.float(), (K,), lw.float(), lb.float(), 1e-5)
+    z = ref_a @ w.float().t() + bias.float()
+    ref_y = {0: z, 1: torch.nn.functional.gelu(z, approximate="tanh"), 2: torch.relu(z)}[act]
+    torch.testing.assert_close(y.float(), ref_y, atol=6e-2, rtol=3e-2)

@@ -211,6 +211,25 @@ MIFT_HD void mift_st_sc1(float2* p, float2 v) {
       (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32);
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The same hand-off for a group of n blocks sharing one counter (e.g. the K-splits of one output
+// tile): true in every thread of the group's n-th arriving block, which has taken the acquire.
+MIFT_HD bool mift_group_arrival(unsigned* counter, unsigned n, int* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int last = 0;
+    if (__hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      last = 1;
+    }
+    *flag_lds = last;
+  }
+  __syncthreads();
+  return *flag_lds != 0;
+}
+
 constexpr int MIFT_ARRIVE_INTS = 9 * 32;
 MIFT_HD bool mift_last_block_arrival(unsigned* counters, int* flag_lds) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done

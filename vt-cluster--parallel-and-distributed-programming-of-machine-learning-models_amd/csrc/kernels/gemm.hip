@@ -1099,19 +1099,62 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
 // chunks: bias, LoRA K-extension (one more k-step), pre-add, pre-activation store, forward activation,
 // residual, and the next adapter's input projection as per-column-tile fp32 slabs (proj_reduce_kernel).
 // Not for dropout (training) or activation-backward epilogues: those keep the tiled kernels.
-template <typename T, int BN, int NW>
+// LNP: A is the raw residual stream and the block applies LayerNorm(A; lnw, lnb, eps) on the fly —
+// row statistics first (two-pass, as ln_fwd8_kernel), then every A fragment normalised and rounded
+// to 16 bits before its MFMA: the decode step's separate LN launches (13 per distilgpt2 step) go away.
+template <typename T, int BN, int NW, bool LNP>
 __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                               T* __restrict__ C, const T* __restrict__ A2,
                                                               const T* __restrict__ B2, int M, int N, int K, int lda,
-                                                              int ldb, int ldc, EpiArgs ep) {
+                                                              int ldb, int ldc, EpiArgs ep, const T* __restrict__ lnw,
+                                                              const T* __restrict__ lnb, float eps) {
   constexpr int NT = BN / 16;  // 16-column MFMA tiles per block
   constexpr int RLD = BN + 4;  // LDS row pitch (floats) of the partial tiles
   __shared__ __attribute__((aligned(16))) float red[NW][64][RLD];
   __shared__ __attribute__((aligned(16))) float ot[64][BN + 1];  // rounded output tile (projection)
+  __shared__ float2 lstat[LNP ? 64 : 1];                         // (mean, rstd) per row
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const int n0 = blockIdx.x * BN;
+  float mrow[4], rrow[4];
+  if constexpr (LNP) {
+    // wave w: rows w, w + NW, ...; lane l: 16-B chunks l, l + 64 (K <= 1024)
+    const int nch = K / 8;
+    for (int r = w; r < 64; r += NW) {
+      const T* xr = A + (size_t)min(r, M - 1) * lda;
+      float v[2][8];
+      float sm = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = lane + u * 64;
+        if (c < nch) load8<T>(xr + c * 8, v[u]);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sm += v[u][e];
+      }
+      const float mean = wave_sum(sm) / K;
+      float q = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (lane + u * 64 >= nch) continue;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float d = v[u][e] - mean; q += d * d; }
+      }
+      const float rstd = rsqrtf(wave_sum(q) / K + eps);
+      if (lane == 0) lstat[r] = make_float2(mean, rstd);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float2 st = lstat[i * 16 + fr];
+      mrow[i] = st.x;
+      rrow[i] = st.y;
+    }
+  }
   float4_ acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1133,6 +1176,27 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const frag_t<T>*>(ap[i] + k);
 #pragma unroll
     for (int j = 0; j < NT; ++j) bf[j] = *reinterpret_cast<const frag_t<T>*>(bp[j] + k);
+    if constexpr (LNP) {
+      float wv[8], bv[8];
+      load8<T>(lnw + k + fq * 8, wv);
+      load8<T>(lnb + k + fq * 8, bv);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        short8 raw;
+        __builtin_memcpy(&raw, &af[i], 16);
+        float x[8];
+        unpack8<T>(raw, x);
+        short8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const T t = (T)((x[e] - mrow[i]) * rrow[i] * wv[e] + bv[e]);
+          short h;
+          __builtin_memcpy(&h, &t, 2);
+          o[e] = h;
+        }
+        __builtin_memcpy(&af[i], &o, 16);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1227,7 +1291,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
 
 template <typename T, int BN, int NW>
 void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
-                   int K, const EpiArgs& ep, hipStream_t st) {
+                   int K, const EpiArgs& ep, hipStream_t st, const T* lnw = nullptr, const T* lnb = nullptr,
+                   float eps = 0.f) {
   const int nb = (N + BN - 1) / BN;
   EpiArgs epx = ep;
   at::Tensor slab;
@@ -1236,9 +1301,14 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     slab = at::empty({(int64_t)nb * M * PW}, a.options().dtype(at::kFloat));
     epx.pws = slab.data_ptr<float>();
   }
-  hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW>), dim3(nb), dim3(NW * 64), 0, st, (const T*)a.data_ptr(),
-                     (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0),
-                     (int)c.stride(0), epx);
+  if (lnw != nullptr)
+    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, true>), dim3(nb), dim3(NW * 64), 0, st, (const T*)a.data_ptr(),
+                       (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0),
+                       (int)c.stride(0), epx, lnw, lnb, eps);
+  else
+    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, false>), dim3(nb), dim3(NW * 64), 0, st, (const T*)a.data_ptr(),
+                       (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0),
+                       (int)c.stride(0), epx, (const T*)nullptr, (const T*)nullptr, 0.f);
   if (ep.pw != nullptr)
     hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
                        (const float*)epx.pws, nb, M, PW, ep.palpha, (T*)ep.pout);
@@ -1446,9 +1516,11 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   const int grid = ntm * ntn;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
                      (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
-  // <= 2 blocks per CU, each wave several rows: few arrivals for the in-launch loss sum
+  // ~4 blocks per CU (2 rows per wave at distilgpt2's M = 8192): the rows of a wave are a dependent
+  // chain of stats loads, so fewer, fatter blocks ran slower (512 blocks of 4 rows per wave: 19 us vs
+  // 9.4 us for one row per wave), while the two-level arrival counters keep 1024 arrivals cheap
   const int rows4 = (M + 3) / 4;
-  const int rpw = (rows4 + 2 * num_cus() - 1) / (2 * num_cus());
+  const int rpw = (rows4 + 4 * num_cus() - 1) / (4 * num_cus());
   const int lgrid = (rows4 + rpw - 1) / rpw;
   at::Tensor total, part;
   if (ws) {
@@ -1674,4 +1746,47 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     TORCH_CHECK(false, "gemm_nt: bf16/fp16 only");
   }
   return {c, pre, proj};
+}
+
+// out [M, N] = act(LayerNorm(x) · wᵀ + bias) for M <= 64 (decode): the skinny kernel with its LN prologue
+// (no normalised copy of x, no LN launch).  The caller checks mift_gemm_ln_ok (else LN + gemm_nt).
+bool mift_gemm_ln_ok(int64_t M, int64_t N, int64_t K) { return M >= 1 && M <= 64 && N % 16 == 0 && N <= 4096 &&
+                                                               K % 64 == 0 && K <= 1024; }
+
+std::vector<at::Tensor> mift_gemm_ln(const at::Tensor& x, const at::Tensor& ln_w, const at::Tensor& ln_b, double eps,
+                                     const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
+                                     bool want_preact) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "gemm_ln: x [M,K], w [N,K]");
+  TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1 && x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_ln: layouts");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && ln_w.scalar_type() == x.scalar_type() &&
+                  ln_b.scalar_type() == x.scalar_type() && ln_w.numel() == x.size(1) && ln_b.numel() == x.size(1) &&
+                  ln_w.is_contiguous() && ln_b.is_contiguous(),
+              "gemm_ln: LN weights of x's dtype, [K]");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(mift_gemm_ln_ok(M, N, K), "gemm_ln: M <= 64, N % 16 == 0, N <= 4096, K % 64 == 0, K <= 1024");
+  TORCH_CHECK(act == ACT_NONE || act == ACT_GELU_TANH || act == ACT_RELU || act == ACT_GELU_ERF, "gemm_ln: forward act");
+  at::Tensor c = at::empty({M, N}, x.options());
+  at::Tensor pre;
+  EpiArgs ep{};
+  ep.alpha = 1.f;
+  ep.act = (int)act;
+  if (bias) {
+    TORCH_CHECK(bias->numel() == N, "gemm_ln: bias size");
+    ep.bias = bias->data_ptr();
+    ep.bias_f32 = bias->scalar_type() == at::kFloat;
+  }
+  if (want_preact) {
+    pre = at::empty({M, N}, x.options());
+    ep.preact = pre.data_ptr();
+  }
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  if (x.scalar_type() == at::kBFloat16)
+    launch_skinny<bf16, 16, 8>(x, w, c, nullptr, nullptr, M, N, K, ep, st, (const bf16*)ln_w.data_ptr(),
+                               (const bf16*)ln_b.data_ptr(), (float)eps);
+  else {
+    TORCH_CHECK(x.scalar_type() == at::kHalf, "gemm_ln: bf16/fp16");
+    launch_skinny<fp16, 16, 8>(x, w, c, nullptr, nullptr, M, N, K, ep, st, (const fp16*)ln_w.data_ptr(),
+                               (const fp16*)ln_b.data_ptr(), (float)eps);
+  }
+  return {c, pre};
 }

@@ -73,13 +73,15 @@ MIFT_HD frag_t<T> masked_frag(const T* p, uint64_t seed, uint64_t idx0, uint32_t
 // distilgpt2-size M (8192 rows -> 512 blocks, two per CU) so more X bytes are in flight per CU;
 // NTI = 1 when only the first 16 rows of W are non-zero (one adapter, r <= 16): half the MFMAs
 // and W loads of the 32-column product.  KS > 1: every block stores its fp32 partial to ws[kss]
-// with plain stores and lora_proj_reduce sums the KS partials into the 16-bit output (an
-// in-kernel last-block reduction needs a device-scope fence per block, ~3.5 us on gfx950).
+// write-through (sc1) and the LAST of a row block's KS blocks to arrive (counter per row block,
+// common.h mift_group_arrival: no release fence) sums the KS partials in split order into the
+// 16-bit output — no lora_proj_reduce launch (OPT micro-batches ran 7 per layer, 4.7 us each).
+// The round-2 form fenced every block (~3.5 us each) and kept the separate reduction.
 template <typename T, int NW, int MT, int NTI>
 __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict__ X, const T* __restrict__ W,
                                                         T* __restrict__ out, int M, int K, int ldx, float alpha,
                                                         uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep, int KS,
-                                                        float* __restrict__ ws, int wrows) {
+                                                        float* __restrict__ ws, int wrows, unsigned* __restrict__ flags) {
   seed = mift_seed(seed, sstep);
   constexpr int RB = 16 * MT;  // rows per block
   __shared__ float red[NW][RB][33];
@@ -172,27 +174,17 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_kernel(const T* __restrict_
   float* wp = ws + (int64_t)kss * M * 32;
   for (int e = tid; e < RB * 32; e += NW * 64) {
     const int r = e >> 5, c = e & 31;
-    if (m0 + r < M) wp[(int64_t)(m0 + r) * 32 + c] = rsum(r, c);
+    if (m0 + r < M) mift_st_sc1(wp + (int64_t)(m0 + r) * 32 + c, rsum(r, c));
   }
-}
-
-// out[m, c] = alpha * sum_s ws[s, m, c]  (8 outputs per thread, 16-B stores)
-template <typename T>
-__global__ __launch_bounds__(256) void lora_proj_reduce(const float* __restrict__ ws, T* __restrict__ out, int M,
-                                                         int KS, float alpha) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
-  const int64_t n = (int64_t)M * 32;
-  if (i >= n) return;
-  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int s = 0; s < KS; ++s) {
-    const float4 a = *reinterpret_cast<const float4*>(ws + s * n + i);
-    const float4 b = *reinterpret_cast<const float4*>(ws + s * n + i + 4);
-    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-    v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  __shared__ int last;
+  if (!mift_group_arrival(flags + mb, (unsigned)KS, &last)) return;
+  for (int e = tid; e < RB * 32; e += NW * 64) {
+    const int r = e >> 5, c = e & 31;
+    if (m0 + r >= M) continue;
+    float v = 0.f;
+    for (int s = 0; s < KS; ++s) v += ws[((int64_t)s * M + m0 + r) * 32 + c];
+    out[(int64_t)(m0 + r) * 32 + c] = (T)(v * alpha);
   }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] *= alpha;
-  store8<T>(out + i, v);
 }
 
 // ----------------------------------------------------------------- lora_wgrad
@@ -586,6 +578,17 @@ __global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const WgArgs arg
 
 }  // namespace
 
+namespace {
+// persistent per-row-block arrival counters of lora_proj's K-split reduction (zeroed once, re-armed by
+// each row block's last arriver; stream-ordered users; first allocated by an eager call)
+unsigned* lp_flags(int n) {
+  static at::Tensor flags;
+  if (!flags.defined() || flags.numel() < n)
+    flags = at::zeros({std::max<int64_t>(n, 1 << 14)}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA));
+  return reinterpret_cast<unsigned*>(flags.data_ptr<int>());
+}
+}  // namespace
+
 at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha, double p, int64_t seed,
                           int64_t rows) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "lora_proj: x [M,K] row-major");
@@ -615,10 +618,12 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   int KS = mblocks >= 2 * cus ? 1 : std::max(1, std::min(std::max(1, nks / 4), (1024 + mblocks - 1) / mblocks));
   if (ks_env > 0) KS = std::max(1, std::min(ks_env, std::max(1, nks / 4)));  // A/B override
   float* ws = nullptr;
+  unsigned* flags = nullptr;
   at::Tensor wsb;
   if (KS > 1) {
     wsb = at::empty({(int64_t)KS * M * 32}, x.options().dtype(at::kFloat));
     ws = wsb.data_ptr<float>();
+    flags = lp_flags(mblocks);
   }
   const int grid = mblocks * KS;
   const bool one_tile = rows <= 16;
@@ -626,7 +631,7 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
     using T = decltype(tt);
     auto args = std::make_tuple((const T*)x.data_ptr(), (const T*)w.data_ptr(), (T*)out.data_ptr(), M, K,
                                 (int)x.stride(0), (float)alpha * ik, (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws,
-                                (int)rows);
+                                (int)rows, flags);
     auto launch = [&](auto kern) {
       std::apply([&](auto... a) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a...); }, args);
     };
@@ -637,13 +642,6 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   };
   if (x.scalar_type() == at::kBFloat16) go(bf16{});
   else go(fp16{});
-  if (KS > 1) {
-    const int rg = (int)(((int64_t)M * 32 / 8 + 255) / 256);
-    if (x.scalar_type() == at::kBFloat16)
-      lora_proj_reduce<bf16><<<rg, 256, 0, st>>>(ws, (bf16*)out.data_ptr(), M, KS, (float)alpha * ik);
-    else
-      lora_proj_reduce<fp16><<<rg, 256, 0, st>>>(ws, (fp16*)out.data_ptr(), M, KS, (float)alpha * ik);
-  }
   return out;
 }
 

@@ -378,7 +378,22 @@ class LnLinear(torch.autograd.Function):
         return (dx.view(ctx.shp), None, None, None, None, None, None, None, *lg)
 
 
+def _infer_ln_gemm(x, ln, lin):
+    """No autograd, no adapter, <= 64 rows (greedy decode): LN inside the skinny GEMM, or None."""
+    if torch.is_grad_enabled() or lin.lora_params() or x.numel() // x.shape[-1] > 64:
+        return None
+    x2 = _flat(x.contiguous())
+    w = lin.w_nk()
+    if not K.gemm_ln_ok(x2, w, ln.weight):
+        return None
+    return x2, w
+
+
 def ln_linear(x, ln, lin, lora_seed=0, training=True, link=None):
+    fast = _infer_ln_gemm(x, ln, lin)
+    if fast is not None:  # decode: one launch instead of LN + GEMM
+        x2, w = fast
+        return K.gemm_ln(x2, ln.weight, ln.bias, ln.eps, w, lin.bias).view(*x.shape[:-1], w.shape[0])
     return LnLinear.apply(x, ln.weight, ln.bias, lin, ln.eps, lora_seed, training, link, *lin.lora_params())
 
 
@@ -477,6 +492,14 @@ class MLP(torch.autograd.Function):
 
 
 def mlp(h, ln, fc1, fc2, act, p, seed, seed_l1=0, seed_l2=0, training=True):
+    fast = _infer_ln_gemm(h, ln, fc1)
+    if fast is not None and not training:  # decode: LN inside fc1's skinny GEMM, no pre-activation store
+        h2, w1 = fast
+        f = K.gemm_ln(h2, ln.weight, ln.bias, ln.eps, w1, fc1.bias, act=act)
+        lo2 = fc2.lora_ops(h.dtype) if fc2.lora_params() else None
+        T2 = lo2.forward(f, seed_l2, False) if lo2 is not None else None
+        out = K.gemm(f, fc2.w_nk(), fc2.bias, T2, lo2.B32 if lo2 else None, residual=h2)
+        return out.view(h.shape)
     l1, l2 = fc1.lora_params(), fc2.lora_params()
     return MLP.apply(h, ln.weight, ln.bias, fc1, fc2, ln.eps, act, p, seed, seed_l1, seed_l2, training, len(l1),
                      *l1, *l2)

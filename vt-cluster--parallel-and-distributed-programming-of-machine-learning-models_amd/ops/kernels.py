@@ -30,6 +30,19 @@ def gemm(a, b, bias=None, a2=None, b2=None, act=0, aux=None, residual=None, drop
     return res if len(res) > 1 else y
 
 
+def gemm_ln_ok(x, w, ln_w):
+    """The LN-prologue skinny GEMM applies: <= 64 rows (decode), narrow N, K <= 1024, one dtype."""
+    M, K = x.shape
+    return (x.is_cuda and x.dtype == w.dtype == ln_w.dtype and x.stride(1) == 1
+            and C().gemm_ln_ok(int(M), int(w.shape[0]), int(K)))
+
+
+def gemm_ln(x, ln_w, ln_b, eps, w, bias=None, act=0, want_preact=False):
+    """act(LayerNorm(x) @ w.T + bias) in one launch (M <= 64: the decode projections)."""
+    y, pre = C().gemm_ln(x, ln_w, ln_b, float(eps), w, bias, int(act), bool(want_preact))
+    return (y, pre) if want_preact else y
+
+
 def lora_proj(x, w32, alpha=1.0, p=0.0, seed=0, rows=32):
     """[M,32] = alpha * dropout(x) @ w32.T   (w32: [32, K]; only its first ``rows`` rows may be non-zero)."""
     return C().lora_proj(x, w32, float(alpha), float(p), int(seed), int(rows))
