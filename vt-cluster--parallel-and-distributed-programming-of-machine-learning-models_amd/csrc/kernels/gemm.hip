@@ -1110,42 +1110,56 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
                                                               const T* __restrict__ lnb, float eps) {
   constexpr int NT = BN / 16;  // 16-column MFMA tiles per block
   constexpr int RLD = BN + 4;  // LDS row pitch (floats) of the partial tiles
-  __shared__ __attribute__((aligned(16))) float red[NW][64][RLD];
-  __shared__ __attribute__((aligned(16))) float ot[64][BN + 1];  // rounded output tile (projection)
-  __shared__ float2 lstat[LNP ? 64 : 1];                         // (mean, rstd) per row
+  // dynamic LDS: the NW partial tiles, then (projection epilogue only) the rounded output tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  auto red = reinterpret_cast<float(*)[64][RLD]>(smem);
+  auto ot = reinterpret_cast<float(*)[BN + 1]>(smem + (size_t)NW * 64 * RLD * 4);
+  __shared__ float2 lstat[LNP ? 64 : 1];  // (mean, rstd) per row
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const int n0 = blockIdx.x * BN;
   float mrow[4], rrow[4];
   if constexpr (LNP) {
-    // wave w: rows w, w + NW, ...; lane l: 16-B chunks l, l + 64 (K <= 1024)
+    // wave w: rows w + NW·j; lane l: 16-B chunks l, l + 64 (K <= 1024).  A batch of RB rows' loads is
+    // issued before any of their reductions (one row at a time was a chain of dependent load
+    // latencies: 16-17 us per LN-prologue GEMM against 6 us without the prologue)
+    constexpr int RPW = 64 / NW, RB = RPW < 4 ? RPW : 4;
     const int nch = K / 8;
-    for (int r = w; r < 64; r += NW) {
-      const T* xr = A + (size_t)min(r, M - 1) * lda;
-      float v[2][8];
-      float sm = 0.f;
+    for (int j0 = 0; j0 < RPW; j0 += RB) {
+      short8 raw[RB][2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int c = lane + u * 64;
-        if (c < nch) load8<T>(xr + c * 8, v[u]);
-        else {
+      for (int jj = 0; jj < RB; ++jj) {
+        const T* xr = A + (size_t)min(w + NW * (j0 + jj), M - 1) * lda;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+        for (int u = 0; u < 2; ++u)
+          raw[jj][u] = *reinterpret_cast<const short8*>(xr + min(lane + u * 64, nch - 1) * 8);
+      }
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj) {
+        float v[2][8];
+        float sm = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          unpack8<T>(raw[jj][u], v[u]);
+          const bool live = lane + u * 64 < nch;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if (!live) v[u][e] = 0.f;
+            sm += v[u][e];
+          }
         }
+        const float mean = wave_sum(sm) / K;
+        float q = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) sm += v[u][e];
+        for (int u = 0; u < 2; ++u) {
+          if (lane + u * 64 >= nch) continue;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { const float d = v[u][e] - mean; q += d * d; }
+        }
+        const float rstd = rsqrtf(wave_sum(q) / K + eps);
+        if (lane == 0) lstat[w + NW * (j0 + jj)] = make_float2(mean, rstd);
       }
-      const float mean = wave_sum(sm) / K;
-      float q = 0.f;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (lane + u * 64 >= nch) continue;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { const float d = v[u][e] - mean; q += d * d; }
-      }
-      const float rstd = rsqrtf(wave_sum(q) / K + eps);
-      if (lane == 0) lstat[r] = make_float2(mean, rstd);
     }
     __syncthreads();
 #pragma unroll
@@ -1301,14 +1315,26 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     slab = at::empty({(int64_t)nb * M * PW}, a.options().dtype(at::kFloat));
     epx.pws = slab.data_ptr<float>();
   }
+  constexpr int RED = NW * 64 * (BN + 4) * 4, OT = 64 * (BN + 1) * 4;
+  static_assert(RED + OT <= 160 * 1024, "LDS budget");
+  const int smem = RED + (ep.pw != nullptr ? OT : 0);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RED + OT);
+    (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RED + OT);
+    attr = true;
+  }
   if (lnw != nullptr)
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, true>), dim3(nb), dim3(NW * 64), 0, st, (const T*)a.data_ptr(),
-                       (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0),
-                       (int)c.stride(0), epx, lnw, lnb, eps);
+    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, true>), dim3(nb), dim3(NW * 64), smem, st,
+                       (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
+                       (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, lnw, lnb, eps);
   else
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, false>), dim3(nb), dim3(NW * 64), 0, st, (const T*)a.data_ptr(),
-                       (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0),
-                       (int)c.stride(0), epx, (const T*)nullptr, (const T*)nullptr, 0.f);
+    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, false>), dim3(nb), dim3(NW * 64), smem, st,
+                       (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
+                       (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, (const T*)nullptr,
+                       (const T*)nullptr, 0.f);
   if (ep.pw != nullptr)
     hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
                        (const float*)epx.pws, nb, M, PW, ep.palpha, (T*)ep.pout);
@@ -1317,7 +1343,8 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
 // the skinny kernel applies: a forward epilogue without dropout on <= 64 rows (MIFT_GEMM_SKINNY=0: off)
 bool skinny_ok(int M, int N, int K, const EpiArgs& ep) {
   static const int env = [] { const char* e = getenv("MIFT_GEMM_SKINNY"); return e ? atoi(e) : 1; }();
-  if (!env || M > 64 || N % 16 != 0 || N > 4096 || K > 1024) return false;
+  if (!env || M > 64 || N % 16 != 0) return false;
+  if (N > 4096 ? (K > 1024 || N % 64 != 0 || env < 2) : K > (env >= 2 ? 4096 : 1024)) return false;
   if (ep.thr != 0 || ep.ext_thr != 0 || ep.aux != nullptr || ep.lm.dbg != 0) return false;
   if (ep.act != ACT_NONE && ep.act != ACT_GELU_TANH && ep.act != ACT_RELU && ep.act != ACT_GELU_ERF) return false;
   if (ep.pw != nullptr && ep.pthr != 0) return false;
@@ -1344,12 +1371,15 @@ template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
   if (tile == 0 && skinny_ok(M, N, K, ep)) {
-    // decode-sized problems with N <= 4096, K <= 1024: 16-column blocks of 8 waves (48-192 blocks at
-    // the distilgpt2 shapes: c_attn 8.7 -> 5.9 us, c_fc 8.7 -> 6.9).  Every block streams all M x K
-    // activations through its CU, so wide N (the LM head: 32 vs 19.5 us on 128x128 tiles, BN = 32)
-    // and long K (fc2, K = 3072: 16 vs 14 us on the 64x64 split-K path) stay on the tiled kernels
-    // (profiles/r4/decode_skinny_trace.txt).
-    launch_skinny<T, 16, 8>(a, b, c, a2, b2, M, N, K, ep, st);
+    // decode-sized problems: 16-column blocks of 8 waves for K <= 1024 (48-192 blocks at the
+    // distilgpt2 shapes: c_attn 8.7 -> 5.9 us, c_fc 8.7 -> 6.9).  Every block streams all M x K
+    // activations through its CU, so long K (fc2, K = 3072: 16 us on 8 or 16 waves vs 14 on the 64x64
+    // split-K path) and wide N (the LM head: 32-column blocks 32 us, 64-column 26.7, vs 17.7-19.5 on
+    // 128x128 tiles) stay tiled; MIFT_GEMM_SKINNY=2 forces them here (A/B;
+    // profiles/r4/decode_skinny_trace.txt, decode_skinny2_trace.txt)
+    if (N > 4096) launch_skinny<T, 64, 4>(a, b, c, a2, b2, M, N, K, ep, st);
+    else if (K > 1024) launch_skinny<T, 16, 16>(a, b, c, a2, b2, M, N, K, ep, st);
+    else launch_skinny<T, 16, 8>(a, b, c, a2, b2, M, N, K, ep, st);
     return;
   }
   if (tile == 0) {

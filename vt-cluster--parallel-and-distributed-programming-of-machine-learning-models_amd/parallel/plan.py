@@ -34,9 +34,11 @@ GiB = 1 << 30
 
 # ms per sequence of a whole dp1 optimizer step (all layers + embed + head + optimizer), seq 512,
 # 96 sequences per step, fp16, fused HIP path, graph replay: tools/mb_sweep.py on one MI355X
-# (profiles/r4/mb_sweep_opt27b.jsonl, mb_sweep_opt67b.jsonl; round 4, before the small-M kernel work).
+# (profiles/r4/mb_sweep_opt67b.jsonl; OPT-2.7B mb >= 4 re-measured after the round-4 kernel hygiene —
+# in-kernel pad-id ignore and loss sum, two-launch optimizer, in-launch lora_proj reduction:
+# profiles/r4/mb_sweep_opt27b_r4k.jsonl; mb 1, 2 from the first sweep, mb_sweep_opt27b.jsonl).
 MEASURED = {
-    "opt-2.7b": {1: 25.5406, 2: 14.4509, 4: 11.2882, 8: 7.9349, 12: 6.9053, 16: 7.4457, 24: 6.6494, 48: 6.5463},
+    "opt-2.7b": {1: 25.5406, 2: 14.4509, 4: 11.5326, 8: 7.9711, 12: 6.7671, 16: 7.3182, 24: 6.4964, 48: 6.3744},
     "opt-6.7b": {1: 34.2091, 2: 20.8388, 4: 18.9054, 8: 14.9082, 16: 14.7781, 32: 14.7251},
 }
 
