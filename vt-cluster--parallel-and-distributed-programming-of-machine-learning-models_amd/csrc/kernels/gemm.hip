@@ -1114,61 +1114,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
   extern __shared__ __attribute__((aligned(16))) char smem[];
   auto red = reinterpret_cast<float(*)[64][RLD]>(smem);
   auto ot = reinterpret_cast<float(*)[BN + 1]>(smem + (size_t)NW * 64 * RLD * 4);
-  __shared__ float2 lstat[LNP ? 64 : 1];  // (mean, rstd) per row
+  __shared__ float lred[LNP ? 2 : 1][LNP ? NW : 1][64];  // per-wave row partials: sum, then sum of squares
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const int n0 = blockIdx.x * BN;
-  float mrow[4], rrow[4];
-  if constexpr (LNP) {
-    // wave w: rows w + NW·j; lane l: 16-B chunks l, l + 64 (K <= 1024).  A batch of RB rows' loads is
-    // issued before any of their reductions (one row at a time was a chain of dependent load
-    // latencies: 16-17 us per LN-prologue GEMM against 6 us without the prologue)
-    constexpr int RPW = 64 / NW, RB = RPW < 4 ? RPW : 4;
-    const int nch = K / 8;
-    for (int j0 = 0; j0 < RPW; j0 += RB) {
-      short8 raw[RB][2];
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj) {
-        const T* xr = A + (size_t)min(w + NW * (j0 + jj), M - 1) * lda;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          raw[jj][u] = *reinterpret_cast<const short8*>(xr + min(lane + u * 64, nch - 1) * 8);
-      }
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj) {
-        float v[2][8];
-        float sm = 0.f;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          unpack8<T>(raw[jj][u], v[u]);
-          const bool live = lane + u * 64 < nch;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            if (!live) v[u][e] = 0.f;
-            sm += v[u][e];
-          }
-        }
-        const float mean = wave_sum(sm) / K;
-        float q = 0.f;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (lane + u * 64 >= nch) continue;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { const float d = v[u][e] - mean; q += d * d; }
-        }
-        const float rstd = rsqrtf(wave_sum(q) / K + eps);
-        if (lane == 0) lstat[w + NW * (j0 + jj)] = make_float2(mean, rstd);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float2 st = lstat[i * 16 + fr];
-      mrow[i] = st.x;
-      rrow[i] = st.y;
-    }
-  }
   float4_ acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1181,40 +1131,106 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
 #pragma unroll
   for (int j = 0; j < NT; ++j) bp[j] = B + (size_t)min(n0 + j * 16 + fr, N - 1) * ldb + fq * 8;
   const int nks = K / 32;
-  // swapped products (weights first): lane holds out[row i*16 + fr][cols j*16 + 4 fq .. +3]
-#pragma unroll 4
-  for (int ks = w; ks < nks; ks += NW) {
-    const int k = ks * 32;
-    frag_t<T> af[4], bf[NT];
+  if constexpr (LNP) {
+    // LayerNorm prologue (K <= 1024: at most KSM k-steps per wave).  All of the wave's fragments are
+    // loaded first; the row statistics come from THOSE registers — per-lane partial sums over the
+    // wave's k-columns, the 4 k-groups of a row reduced by two lane shuffles, the NW waves through
+    // LDS — two-pass (mean, then squared deviations) as ln_fwd8_kernel; then every fragment is
+    // normalised in place before its MFMA.  The first form re-read whole rows for the statistics,
+    // one dependent load round more (12.7-13.8 us vs 6.2 us for the same GEMM without LN).
+    constexpr int KSM = (1024 / 32 + NW - 1) / NW;
+    frag_t<T> afs[KSM][4], bfs[KSM][NT];
+    float wv[KSM][8], bv[KSM][8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const frag_t<T>*>(ap[i] + k);
+    for (int kk = 0; kk < KSM; ++kk) {
+      const int ks = w + kk * NW;
+      if (ks < nks) {  // wave-uniform
+        const int k = ks * 32;
 #pragma unroll
-    for (int j = 0; j < NT; ++j) bf[j] = *reinterpret_cast<const frag_t<T>*>(bp[j] + k);
-    if constexpr (LNP) {
-      float wv[8], bv[8];
-      load8<T>(lnw + k + fq * 8, wv);
-      load8<T>(lnb + k + fq * 8, bv);
+        for (int i = 0; i < 4; ++i) afs[kk][i] = *reinterpret_cast<const frag_t<T>*>(ap[i] + k);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bfs[kk][j] = *reinterpret_cast<const frag_t<T>*>(bp[j] + k);
+        load8<T>(lnw + k + fq * 8, wv[kk]);
+        load8<T>(lnb + k + fq * 8, bv[kk]);
+      }
+    }
+    float mean[4], rstd[4];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KSM; ++kk) {
+        if (w + kk * NW >= nks) break;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          short8 raw;
+          __builtin_memcpy(&raw, &afs[kk][i], 16);
+          float x[8];
+          unpack8<T>(raw, x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = pass == 0 ? x[e] : x[e] - mean[i];
+            ps[i] += pass == 0 ? d : d * d;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ps[i] += __shfl_xor(ps[i], 16, 64);
+        ps[i] += __shfl_xor(ps[i], 32, 64);
+      }
+      if (fq == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lred[pass][w][i * 16 + fr] = ps[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) t += lred[pass][v][i * 16 + fr];
+        if (pass == 0) mean[i] = t / K;
+        else rstd[i] = rsqrtf(t / K + eps);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < KSM; ++kk) {
+      if (w + kk * NW >= nks) break;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         short8 raw;
-        __builtin_memcpy(&raw, &af[i], 16);
+        __builtin_memcpy(&raw, &afs[kk][i], 16);
         float x[8];
         unpack8<T>(raw, x);
         short8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const T t = (T)((x[e] - mrow[i]) * rrow[i] * wv[e] + bv[e]);
+          const T t = (T)((x[e] - mean[i]) * rstd[i] * wv[kk][e] + bv[kk][e]);
           short h;
           __builtin_memcpy(&h, &t, 2);
           o[e] = h;
         }
-        __builtin_memcpy(&af[i], &o, 16);
+        frag_t<T> af;
+        __builtin_memcpy(&af, &o, 16);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bfs[kk][j], af, acc[i][j]);
       }
     }
+  } else {
+    // swapped products (weights first): lane holds out[row i*16 + fr][cols j*16 + 4 fq .. +3]
+#pragma unroll 4
+    for (int ks = w; ks < nks; ks += NW) {
+      const int k = ks * 32;
+      frag_t<T> af[4], bf[NT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const frag_t<T>*>(ap[i] + k);
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bf[j], af[i], acc[i][j]);
+      for (int j = 0; j < NT; ++j) bf[j] = *reinterpret_cast<const frag_t<T>*>(bp[j] + k);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bf[j], af[i], acc[i][j]);
+    }
   }
   if (A2 != nullptr && w == NW - 1) {  // LoRA K-extension: one more k-step (the wave with the fewest)
     frag_t<T> af2[4], bf2[NT];
@@ -1320,17 +1336,22 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
   const int smem = RED + (ep.pw != nullptr ? OT : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, RED + OT);
+    if constexpr (BN == 16 && NW == 8)
+      (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, RED + OT);
     (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, RED + OT);
     attr = true;
   }
-  if (lnw != nullptr)
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, true>), dim3(nb), dim3(NW * 64), smem, st,
-                       (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
-                       (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, lnw, lnb, eps);
-  else
+  if (lnw != nullptr) {
+    // the LN prologue holds a wave's whole K range in registers: the 16-column, 8-wave form only
+    if constexpr (BN == 16 && NW == 8)
+      hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, true>), dim3(nb), dim3(NW * 64), smem, st,
+                         (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
+                         (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, lnw, lnb, eps);
+    else
+      TORCH_CHECK(false, "gemm_skinny: LN prologue needs the 16-column 8-wave form");
+  } else
     hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, false>), dim3(nb), dim3(NW * 64), smem, st,
                        (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
                        (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, (const T*)nullptr,
