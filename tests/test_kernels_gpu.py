@@ -569,11 +569,13 @@ def test_gemm_skinny_decode_shapes(M, N, K):
 
 
 @pytest.mark.parametrize("rows", [8, 24])
-def test_gemm_skinny_epilogue_projection(rows):
-    """The skinny kernel's next-adapter projection slabs == lora_proj over its stored output."""
+@pytest.mark.parametrize("K", [768, 3072])
+def test_gemm_skinny_epilogue_projection(rows, K):
+    """The skinny kernel's next-adapter projection slabs == lora_proj over its stored output (K = 3072:
+    the K-split form, whose last-arriving block runs the epilogue and the projection)."""
     C = _C()
     torch.manual_seed(9)
-    M, K, N = 64, 768, 3072
+    M, N = 64, 3072
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
     bias = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)

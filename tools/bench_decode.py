@@ -46,7 +46,14 @@ def main():
         col.zero_()
         K.decode_tail(logits, V, done, ids, out, col, pos, t, 0, 50256, 50256)
 
+    for nth in ("256", "512", "1024"):
+        os.environ["MIFT_TAIL_NTH"] = nth
+        rec(f"decode_tail(+col reset) {nth} threads", tail)
+    os.environ.pop("MIFT_TAIL_NTH")
     rec("decode_tail(+col reset)", tail)
+    # the tail's last steps alone: one row's argmax over 64 columns (bookkeeping-bound)
+    rec("decode_tail V=64 (bookkeeping only)", lambda: (col.zero_(), K.decode_tail(logits, 64, done, ids, out, col, pos,
+                                                                                   t, 0, 50256, 50256)))
     rec("col reset alone", lambda: col.zero_())
     rec("torch argmax (float)", lambda: logits.float().argmax(-1))
     x = torch.randn(B, d, device=dev).to(dt)

@@ -173,73 +173,93 @@ namespace {
 // as maximal (torch.argmax); a finished row emits pad; out[b, col[b]] = token; done[b] |= token == eos
 // (eos >= 0); the next step's input ids[b] = done ? fill : token; col, pos advance; block 0 advances
 // the cache position t.  16-B logit loads (row stride % 8 == 0), scalar tail.
-MIFT_HD bool argmax_better(float v, int i, float bv, int bi) {
-  const bool vn = v != v, bn = bv != bv;
-  if (vn != bn) return vn;
-  if (vn) return i < bi;
-  return v > bv || (v == bv && i < bi);
+// Order-preserving integer key of a logit: NaN maximal (torch.argmax), -0 == +0, otherwise the float
+// order.  The first version compared (value, index) with early returns for the NaN cases; hipcc kept
+// them as two divergent branches per element (decode_tail 13.8 us for 64 x 50257 logits): integer keys
+// compile to compares and selects only.
+MIFT_HD int argmax_key(float v) {
+  const int b = __float_as_int(v);
+  const int k = b >= 0 ? b : b ^ 0x7fffffff;
+  return v != v ? 0x7fffffff : (v == 0.f ? 0 : k);
 }
 
-template <typename T>
-__global__ __launch_bounds__(1024) void decode_tail_kernel(const T* __restrict__ logits, int64_t ldl, int V,
+template <typename T, int NTH>
+__global__ __launch_bounds__(NTH) void decode_tail_kernel(const T* __restrict__ logits, int64_t ldl, int V,
                                                           bool* __restrict__ done, int64_t* __restrict__ ids,
                                                           int64_t* __restrict__ out, int max_new,
                                                           int64_t* __restrict__ col, int64_t* __restrict__ pos,
                                                           int* __restrict__ t, int64_t fill, int64_t pad, int64_t eos) {
-  // 16 waves, each thread's chunks loaded in batches of UN before any compare: the loop was a chain
-  // of dependent loads (27 us per step for 64 x 50257 with one load in flight per thread)
-  constexpr int NTH = 1024, UN = 8;
-  __shared__ float sv[NTH / 64];
+  // each thread's chunks loaded in batches of UN before any compare (one load in flight per thread
+  // was a chain of dependent loads); a thread visits its elements in increasing index order, so a
+  // strictly greater key keeps the first maximum; lanes and waves then tie-break on the index
+  constexpr int UN = 8;
+  __shared__ int sk[NTH / 64];
   __shared__ int si[NTH / 64];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const T* row = logits + (int64_t)b * ldl;
-  float best = -INFINITY;
-  int bi = 0x7fffffff;
+  int bk = (int)0x80000000, bi = 0x7fffffff;
   const int nv = V / 8;
+  // this row's bookkeeping inputs, requested before the scan (consumed by thread 0 at the end)
+  bool d0 = false;
+  int64_t c = 0, p0 = 0;
+  int t0 = 0;
+  if (tid == 0) {
+    d0 = done[b];
+    c = col[b];
+    p0 = pos[b];
+    if (b == 0) t0 = t[0];
+  }
   for (int c0 = tid; c0 < nv; c0 += NTH * UN) {
     short8 v[UN];
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
-      const int c = min(c0 + u * NTH, nv - 1);  // clamped: a repeated chunk never wins (same index)
-      v[u] = *reinterpret_cast<const short8*>(row + (int64_t)c * 8);
+      const int ch = min(c0 + u * NTH, nv - 1);  // clamped: a repeated chunk never wins (not greater)
+      v[u] = *reinterpret_cast<const short8*>(row + (int64_t)ch * 8);
     }
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
-      const int c = c0 + u * NTH;
-      if (c >= nv) break;
       float f[8];
       unpack8<T>(v[u], f);
+      const int base = min(c0 + u * NTH, nv - 1) * 8;
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (argmax_better(f[e], c * 8 + e, best, bi)) { best = f[e]; bi = c * 8 + e; }
+      for (int e = 0; e < 8; ++e) {
+        const int k = argmax_key(f[e]);
+        const bool gt = k > bk;
+        bk = gt ? k : bk;
+        bi = gt ? base + e : bi;
+      }
     }
   }
   for (int j = nv * 8 + tid; j < V; j += NTH) {
-    const float v = (float)row[j];
-    if (argmax_better(v, j, best, bi)) { best = v; bi = j; }
+    const int k = argmax_key((float)row[j]);
+    const bool gt = k > bk;
+    bk = gt ? k : bk;
+    bi = gt ? j : bi;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+    const int ok = __shfl_xor(bk, o, 64), oi = __shfl_xor(bi, o, 64);
+    const bool bt = ok > bk || (ok == bk && oi < bi);
+    bk = bt ? ok : bk;
+    bi = bt ? oi : bi;
   }
-  if (lane == 0) { sv[w] = best; si[w] = bi; }
+  if (lane == 0) { sk[w] = bk; si[w] = bi; }
   __syncthreads();
   if (tid == 0) {
 #pragma unroll
-    for (int k = 1; k < NTH / 64; ++k)
-      if (argmax_better(sv[k], si[k], best, bi)) { best = sv[k]; bi = si[k]; }
-    const bool d0 = done[b];
+    for (int q = 1; q < NTH / 64; ++q) {
+      const bool bt = sk[q] > bk || (sk[q] == bk && si[q] < bi);
+      bk = bt ? sk[q] : bk;
+      bi = bt ? si[q] : bi;
+    }
     const int64_t tok = d0 ? pad : (int64_t)bi;
-    const int64_t c = col[b];
     if (c >= 0 && c < max_new) out[(int64_t)b * max_new + c] = tok;
     const bool d = d0 || (eos >= 0 && tok == eos);
     done[b] = d;
     ids[b] = d ? fill : tok;
     col[b] = c + 1;
-    pos[b] += 1;
-    if (b == 0) t[0] += 1;
+    pos[b] = p0 + 1;
+    if (b == 0) t[0] = t0 + 1;
   }
 }
 
@@ -262,10 +282,18 @@ void mift_decode_tail(const at::Tensor& logits, int64_t V, at::Tensor& done, at:
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   auto launch = [&](auto tag) {
     using T = decltype(tag);
-    decode_tail_kernel<T><<<(unsigned)B, 1024, 0, st>>>(
-        reinterpret_cast<const T*>(logits.data_ptr()), logits.stride(0), (int)V, done.data_ptr<bool>(),
-        ids.data_ptr<int64_t>(), out.data_ptr<int64_t>(), (int)out.size(1), col.data_ptr<int64_t>(),
-        pos.data_ptr<int64_t>(), t.data_ptr<int>(), fill, pad, eos);
+    // block size: MIFT_TAIL_NTH (A/B, read per call) — 256 / 512 / 1024 threads per row
+    const char* e = getenv("MIFT_TAIL_NTH");
+    const int nth = e ? atoi(e) : 1024;
+    auto go = [&](auto kern, int threads) {
+      kern<<<(unsigned)B, threads, 0, st>>>(
+          reinterpret_cast<const T*>(logits.data_ptr()), logits.stride(0), (int)V, done.data_ptr<bool>(),
+          ids.data_ptr<int64_t>(), out.data_ptr<int64_t>(), (int)out.size(1), col.data_ptr<int64_t>(),
+          pos.data_ptr<int64_t>(), t.data_ptr<int>(), fill, pad, eos);
+    };
+    if (nth == 256) go(decode_tail_kernel<T, 256>, 256);
+    else if (nth == 512) go(decode_tail_kernel<T, 512>, 512);
+    else go(decode_tail_kernel<T, 1024>, 1024);
   };
   if (logits.scalar_type() == at::kBFloat16) launch(bf16{});
   else {

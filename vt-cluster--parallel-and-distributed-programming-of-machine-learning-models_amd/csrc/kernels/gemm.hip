@@ -1107,7 +1107,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
                                                               T* __restrict__ C, const T* __restrict__ A2,
                                                               const T* __restrict__ B2, int M, int N, int K, int lda,
                                                               int ldb, int ldc, EpiArgs ep, const T* __restrict__ lnw,
-                                                              const T* __restrict__ lnb, float eps) {
+                                                              const T* __restrict__ lnb, float eps, int ksplit,
+                                                              float* __restrict__ kws, unsigned* __restrict__ kflags) {
   constexpr int NT = BN / 16;  // 16-column MFMA tiles per block
   constexpr int RLD = BN + 4;  // LDS row pitch (floats) of the partial tiles
   // dynamic LDS: the NW partial tiles, then (projection epilogue only) the rounded output tile
@@ -1118,7 +1119,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const int n0 = blockIdx.x * BN;
+  // ksplit > 1 (long K, e.g. fc2's 3072): the ksplit blocks of a column tile take equal k ranges and the
+  // last to arrive sums their fp32 partials in split order before the epilogue (write-through partials,
+  // one counter per tile: common.h mift_group_arrival)
+  const int tile = blockIdx.x / ksplit, sidx = blockIdx.x - tile * ksplit;
+  const int n0 = tile * BN;
   float4_ acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1130,7 +1135,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
   for (int i = 0; i < 4; ++i) ap[i] = A + (size_t)min(i * 16 + fr, M - 1) * lda + fq * 8;
 #pragma unroll
   for (int j = 0; j < NT; ++j) bp[j] = B + (size_t)min(n0 + j * 16 + fr, N - 1) * ldb + fq * 8;
-  const int nks = K / 32;
+  const int kper = K / 32 / ksplit, kb0 = sidx * kper, nks = kb0 + kper;
   if constexpr (LNP) {
     // LayerNorm prologue (K <= 1024: at most KSM k-steps per wave).  All of the wave's fragments are
     // loaded first; the row statistics come from THOSE registers — per-lane partial sums over the
@@ -1219,7 +1224,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
   } else {
     // swapped products (weights first): lane holds out[row i*16 + fr][cols j*16 + 4 fq .. +3]
 #pragma unroll 4
-    for (int ks = w; ks < nks; ks += NW) {
+    for (int ks = kb0 + w; ks < nks; ks += NW) {
       const int k = ks * 32;
       frag_t<T> af[4], bf[NT];
 #pragma unroll
@@ -1232,7 +1237,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bf[j], af[i], acc[i][j]);
     }
   }
-  if (A2 != nullptr && w == NW - 1) {  // LoRA K-extension: one more k-step (the wave with the fewest)
+  if (A2 != nullptr && w == NW - 1 && sidx == ksplit - 1) {  // LoRA K-extension: one more k-step
     frag_t<T> af2[4], bf2[NT];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1253,20 +1258,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
   __syncthreads();
   const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
   constexpr int CPR = BN / 8;  // 8-column chunks per row
-  for (int ch = tid; ch < 64 * CPR; ch += NW * 64) {
-    const int row = ch / CPR, c8 = (ch % CPR) * 8;
+  auto finish = [&](int row, int c8, float* z) {
     const int gn = n0 + c8;
-    if (row >= M || gn >= N) continue;
-    float z[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) z[e] = 0.f;
-#pragma unroll
-    for (int v = 0; v < NW; ++v) {
-      const float4 p0 = *reinterpret_cast<const float4*>(&red[v][row][c8]);
-      const float4 p1 = *reinterpret_cast<const float4*>(&red[v][row][c8 + 4]);
-      z[0] += p0.x; z[1] += p0.y; z[2] += p0.z; z[3] += p0.w;
-      z[4] += p1.x; z[5] += p1.y; z[6] += p1.z; z[7] += p1.w;
-    }
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (ep.bias != nullptr) {
       if (ep.bias_f32) {
@@ -1301,12 +1294,50 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
 #pragma unroll
       for (int e = 0; e < 8; ++e) ot[row][c8 + e] = (float)(T)z[e];
     }
+  };
+  for (int ch = tid; ch < 64 * CPR; ch += NW * 64) {
+    const int row = ch / CPR, c8 = (ch % CPR) * 8;
+    if (row >= M || n0 + c8 >= N) continue;
+    float z[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = 0.f;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+      const float4 p0 = *reinterpret_cast<const float4*>(&red[v][row][c8]);
+      const float4 p1 = *reinterpret_cast<const float4*>(&red[v][row][c8 + 4]);
+      z[0] += p0.x; z[1] += p0.y; z[2] += p0.z; z[3] += p0.w;
+      z[4] += p1.x; z[5] += p1.y; z[6] += p1.z; z[7] += p1.w;
+    }
+    if (ksplit > 1) {
+      float* dst = kws + (((size_t)tile * ksplit + sidx) * 64 + row) * BN + c8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mift_st_sc1(dst + e, z[e]);
+      continue;
+    }
+    finish(row, c8, z);
+  }
+  if (ksplit > 1) {
+    __shared__ int klast;
+    if (!mift_group_arrival(kflags + tile, (unsigned)ksplit, &klast)) return;
+    for (int ch = tid; ch < 64 * CPR; ch += NW * 64) {
+      const int row = ch / CPR, c8 = (ch % CPR) * 8;
+      if (row >= M || n0 + c8 >= N) continue;
+      float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < ksplit; ++q) {
+        const float* src = kws + (((size_t)tile * ksplit + q) * 64 + row) * BN + c8;
+        const float4 p0 = *reinterpret_cast<const float4*>(src);
+        const float4 p1 = *reinterpret_cast<const float4*>(src + 4);
+        z[0] += p0.x; z[1] += p0.y; z[2] += p0.z; z[3] += p0.w;
+        z[4] += p1.x; z[5] += p1.y; z[6] += p1.z; z[7] += p1.w;
+      }
+      finish(row, c8, z);
+    }
   }
   if (ep.pws == nullptr) return;  // block-uniform
   // next adapter's input projection over this block's columns: slab[blockIdx][row][j]
   __syncthreads();
   const int PW = ep.prow <= 16 ? 16 : 32;
-  float* slab = ep.pws + (size_t)blockIdx.x * M * PW;
+  float* slab = ep.pws + (size_t)tile * M * PW;
   const T* pw = reinterpret_cast<const T*>(ep.pw);
   for (int idx = tid; idx < M * PW; idx += NW * 64) {
     const int r = idx / PW, j = idx % PW;
@@ -1319,11 +1350,28 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
   }
 }
 
+// persistent per-column-tile arrival counters of the skinny kernel's K split (zeroed once, re-armed
+// by each tile's last arriver; stream-ordered users; first allocated by an eager call)
+unsigned* skinny_flags(int n) {
+  static at::Tensor flags;
+  if (!flags.defined() || flags.numel() < n)
+    flags = at::zeros({std::max<int64_t>(n, 1 << 12)}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA));
+  return reinterpret_cast<unsigned*>(flags.data_ptr<int>());
+}
+
 template <typename T, int BN, int NW>
 void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, const T* lnw = nullptr, const T* lnb = nullptr,
-                   float eps = 0.f) {
+                   float eps = 0.f, int ksplit = 1) {
   const int nb = (N + BN - 1) / BN;
+  at::Tensor kwsb;
+  float* kws = nullptr;
+  unsigned* kflags = nullptr;
+  if (ksplit > 1) {
+    kwsb = at::empty({(int64_t)nb * ksplit * 64 * BN}, a.options().dtype(at::kFloat));
+    kws = kwsb.data_ptr<float>();
+    kflags = skinny_flags(nb);
+  }
   EpiArgs epx = ep;
   at::Tensor slab;
   const int PW = ep.prow <= 16 ? 16 : 32;
@@ -1348,14 +1396,15 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     if constexpr (BN == 16 && NW == 8)
       hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, true>), dim3(nb), dim3(NW * 64), smem, st,
                          (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
-                         (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, lnw, lnb, eps);
+                         (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, lnw, lnb, eps, 1,
+                         (float*)nullptr, (unsigned*)nullptr);
     else
       TORCH_CHECK(false, "gemm_skinny: LN prologue needs the 16-column 8-wave form");
   } else
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, false>), dim3(nb), dim3(NW * 64), smem, st,
+    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, false>), dim3(nb * ksplit), dim3(NW * 64), smem, st,
                        (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
                        (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, (const T*)nullptr,
-                       (const T*)nullptr, 0.f);
+                       (const T*)nullptr, 0.f, ksplit, kws, kflags);
   if (ep.pw != nullptr)
     hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
                        (const float*)epx.pws, nb, M, PW, ep.palpha, (T*)ep.pout);
@@ -1365,7 +1414,7 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
 bool skinny_ok(int M, int N, int K, const EpiArgs& ep) {
   static const int env = [] { const char* e = getenv("MIFT_GEMM_SKINNY"); return e ? atoi(e) : 1; }();
   if (!env || M > 64 || N % 16 != 0) return false;
-  if (N > 4096 ? (K > 1024 || N % 64 != 0 || env < 2) : K > (env >= 2 ? 4096 : 1024)) return false;
+  if (N > 4096 ? (K > 1024 || N % 64 != 0 || env < 2) : (K > 4096 || (K > 1024 && (K / 32) % ((K + 1023) / 1024)))) return false;
   if (ep.thr != 0 || ep.ext_thr != 0 || ep.aux != nullptr || ep.lm.dbg != 0) return false;
   if (ep.act != ACT_NONE && ep.act != ACT_GELU_TANH && ep.act != ACT_RELU && ep.act != ACT_GELU_ERF) return false;
   if (ep.pw != nullptr && ep.pthr != 0) return false;
@@ -1392,15 +1441,14 @@ template <typename T>
 void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, int tile) {
   if (tile == 0 && skinny_ok(M, N, K, ep)) {
-    // decode-sized problems: 16-column blocks of 8 waves for K <= 1024 (48-192 blocks at the
-    // distilgpt2 shapes: c_attn 8.7 -> 5.9 us, c_fc 8.7 -> 6.9).  Every block streams all M x K
-    // activations through its CU, so long K (fc2, K = 3072: 16 us on 8 or 16 waves vs 14 on the 64x64
-    // split-K path) and wide N (the LM head: 32-column blocks 32 us, 64-column 26.7, vs 17.7-19.5 on
-    // 128x128 tiles) stay tiled; MIFT_GEMM_SKINNY=2 forces them here (A/B;
-    // profiles/r4/decode_skinny_trace.txt, decode_skinny2_trace.txt)
+    // decode-sized problems: 16-column blocks of 8 waves (48-192 blocks at the distilgpt2 shapes:
+    // c_attn 8.7 -> 5.9 us, c_fc 8.7 -> 6.9).  Every block streams its rows' K range through its CU, so
+    // long K is split over (K + 1023) / 1024 blocks per column tile, reduced by the last to arrive
+    // (fc2, K = 3072: one block per tile ran 16 us on 8 or 16 waves vs 14 on the 64x64 split-K path);
+    // wide N (the LM head: 32-column blocks 32 us, 64-column 26.7, vs 17.7-19.5 on 128x128 tiles) stays
+    // tiled unless MIFT_GEMM_SKINNY=2 (A/B; profiles/r4/decode_skinny_trace.txt, decode_skinny2_trace.txt)
     if (N > 4096) launch_skinny<T, 64, 4>(a, b, c, a2, b2, M, N, K, ep, st);
-    else if (K > 1024) launch_skinny<T, 16, 16>(a, b, c, a2, b2, M, N, K, ep, st);
-    else launch_skinny<T, 16, 8>(a, b, c, a2, b2, M, N, K, ep, st);
+    else launch_skinny<T, 16, 8>(a, b, c, a2, b2, M, N, K, ep, st, nullptr, nullptr, 0.f, (K + 1023) / 1024);
     return;
   }
   if (tile == 0) {
