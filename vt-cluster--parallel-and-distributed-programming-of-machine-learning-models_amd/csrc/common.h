@@ -62,6 +62,7 @@ typedef _Float16 fp16;
 typedef short short8 __attribute__((ext_vector_type(8)));
 typedef short short4_ __attribute__((ext_vector_type(4)));
 typedef float float4_ __attribute__((ext_vector_type(4)));
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
 typedef float float16_ __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 fp16x8 __attribute__((ext_vector_type(8)));
@@ -231,6 +232,16 @@ MIFT_HD bool mift_group_arrival(unsigned* counter, unsigned n, int* flag_lds) {
 }
 
 constexpr int MIFT_ARRIVE_INTS = 9 * 32;
+// 16-B write-through store: a buffer store with the sc1 bit (aux 16) at byte offset `off` of the
+// buffer at `base` (wave-uniform), for hand-offs of tiles (the dword stores of mift_st_sc1 cost ~6x
+// per byte).
+MIFT_HD void mift_st16_sc1(float* base, uint32_t off, float4_ v) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  v4u32 u;
+  __builtin_memcpy(&u, &v, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(u, rsrc, (int)off, 0, 16);
+}
+
 MIFT_HD bool mift_last_block_arrival(unsigned* counters, int* flag_lds) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done
   __syncthreads();                                    // ... and every other wave's

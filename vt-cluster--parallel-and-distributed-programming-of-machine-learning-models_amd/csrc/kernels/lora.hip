@@ -241,6 +241,11 @@ template <int NQT>
 MIFT_HD void wg_store(const WgArgs& args, const WgProb& pr, const float4_ (&acc)[NQT], int p0, int wave, int g, int li) {
   if (args.ws != nullptr) {  // deterministic: slab [c][li][64 rows of p], one 16-B store per (c)
     float* slab = args.ws + (size_t)blockIdx.x * (NQT * 16 * 64);
+    if (args.flags != nullptr) {  // in-launch reduction: write-through, handed to the tile's last block
+#pragma unroll
+      for (int c = 0; c < NQT; ++c) mift_st16_sc1(slab, ((c * 16 + li) * 64 + wave * 16 + g * 4) * 4, acc[c]);
+      return;
+    }
 #pragma unroll
     for (int c = 0; c < NQT; ++c)
       *reinterpret_cast<float4_*>(slab + (c * 16 + li) * 64 + wave * 16 + g * 4) = acc[c];
@@ -508,21 +513,12 @@ __global__ __launch_bounds__(256) void lora_wgrad2_kernel(const WgArgs args) {
   }
   wg_store<NQT>(args, pr, acc, p0, wave, g, li);
   if (args.flags != nullptr) {  // the last chunk block of this column tile reduces its slabs
+    // write-through slabs + relaxed arrival + one acquire in the last block (common.h); round 3's form
+    // fenced every block (__threadfence in all threads + an acq_rel atomic): step 5.09 -> 6.74 ms
     __shared__ int last;
-    __threadfence();  // this block's slab stores are visible device-wide before it arrives
-    __syncthreads();
-    if (tid == 0) {
-      const int nch = (M + rows_per_block - 1) / rows_per_block;
-      int* f = args.flags + pr.tile0 + pt;
-      const int prev = __hip_atomic_fetch_add(f, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      last = prev == nch - 1;
-      if (last) __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-    }
-    __syncthreads();
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other chunks' slabs
+    const int nch = (M + rows_per_block - 1) / rows_per_block;
+    if (mift_group_arrival(reinterpret_cast<unsigned*>(args.flags + pr.tile0 + pt), (unsigned)nch, &last))
       wg_reduce_tile<NQT>(args, pr, pt);
-    }
   }
 }
 
@@ -690,10 +686,10 @@ void launch_wgrad(WgArgs& args, hipStream_t st) {
       args.p[i].tile0 = tiles;
       tiles += args.p[i].P / 64;
     }
-    // MIFT_WGRAD_FIN=1 (opt-in, measured much slower): the last chunk block of every column tile
-    // reduces in place instead of a second launch.  Every block then needs an agent-scope release
-    // (its slab visible to the finisher on another XCD), which on the multi-XCD MI355X writes back
-    // the XCD's L2: the distilgpt2 step went 5.09 -> 6.74 ms (profiles/r3/step_ab_wgrad_finisher_rejected.jsonl).
+    // MIFT_WGRAD_FIN=1 (opt-in): the last chunk block of every column tile reduces in place instead of
+    // a second launch.  Round 3's form gave every block an agent-scope release (L2 write-back of its
+    // XCD): step 5.09 -> 6.74 ms (profiles/r3/step_ab_wgrad_finisher_rejected.jsonl); round 4 stores the
+    // slabs write-through and counts arrivals relaxed (common.h mift_group_arrival).
     const char* fe = getenv("MIFT_WGRAD_FIN");
     const bool fin = !v1 && fe && atoi(fe) == 1;
     args.flags = fin ? wg_flags(tiles) : nullptr;
