@@ -610,8 +610,11 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
   const int MT = mte ? (atoi(mte) == 1 ? 1 : 2) : ((M + 31) / 32 >= 2 * cus ? 2 : 1);
   const int mblocks = (M + 16 * MT - 1) / (16 * MT), nks = K / 32;
   static const int ks_env = [] { const char* e = getenv("MIFT_LORA_KS"); return e ? atoi(e) : 0; }();
-  // K-splits only when the row blocks alone leave CUs idle (>= ~1024 blocks, >= 4 k-steps each)
-  int KS = mblocks >= 2 * cus ? 1 : std::max(1, std::min(std::max(1, nks / 4), (1024 + mblocks - 1) / mblocks));
+  // K-splits only when the row blocks alone leave CUs idle (>= ~1024 blocks, >= 4 k-steps each).  With
+  // at least one row block per CU the split's hand-off costs more than the extra blocks give: OPT-2.7B
+  // at micro-batch 12 (M = 6144, 384 row blocks, K = 2560) ran its projections at 22.3 / 39.1 us with
+  // KS = 3 and 19.4 / 35.2 us unsplit, step 675 -> 669 ms (profiles/r4/lora_proj_ks_opt27b_mb12.txt)
+  int KS = mblocks >= cus ? 1 : std::max(1, std::min(std::max(1, nks / 4), (1024 + mblocks - 1) / mblocks));
   if (ks_env > 0) KS = std::max(1, std::min(ks_env, std::max(1, nks / 4)));  // A/B override
   float* ws = nullptr;
   unsigned* flags = nullptr;
