@@ -631,13 +631,22 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
     auto args = std::make_tuple((const T*)x.data_ptr(), (const T*)w.data_ptr(), (T*)out.data_ptr(), M, K,
                                 (int)x.stride(0), (float)alpha * ik, (uint64_t)seed, mift_seed_step(), thr, ik, KS, ws,
                                 (int)rows, flags);
-    auto launch = [&](auto kern) {
-      std::apply([&](auto... a) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a...); }, args);
+    auto launch = [&](auto kern, int threads) {
+      std::apply([&](auto... a) { hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, st, a...); }, args);
     };
-    if (MT == 1 && one_tile) launch(lora_proj_kernel<T, 4, 1, 1>);
-    else if (MT == 1) launch(lora_proj_kernel<T, 4, 1, 2>);
-    else if (one_tile) launch(lora_proj_kernel<T, 4, 2, 1>);
-    else launch(lora_proj_kernel<T, 4, 2, 2>);
+    // MIFT_LORA_NW=8 (A/B only): 8-wave blocks, each wave half the k-steps — measured slower at OPT-2.7B
+    // mb 12 (20.7 / 37.8 vs 19.4 / 35.2 us, step 647 vs 644 ms: profiles/r4/lora_proj_nw8_rejected.txt)
+    static const int nw_env = [] { const char* e = getenv("MIFT_LORA_NW"); return e ? atoi(e) : 0; }();
+    const bool nw8 = nw_env == 8;
+    if (nw8) {
+      if (MT == 1 && one_tile) launch(lora_proj_kernel<T, 8, 1, 1>, 512);
+      else if (MT == 1) launch(lora_proj_kernel<T, 8, 1, 2>, 512);
+      else if (one_tile) launch(lora_proj_kernel<T, 8, 2, 1>, 512);
+      else launch(lora_proj_kernel<T, 8, 2, 2>, 512);
+    } else if (MT == 1 && one_tile) launch(lora_proj_kernel<T, 4, 1, 1>, 256);
+    else if (MT == 1) launch(lora_proj_kernel<T, 4, 1, 2>, 256);
+    else if (one_tile) launch(lora_proj_kernel<T, 4, 2, 1>, 256);
+    else launch(lora_proj_kernel<T, 4, 2, 2>, 256);
   };
   if (x.scalar_type() == at::kBFloat16) go(bf16{});
   else go(fp16{});
