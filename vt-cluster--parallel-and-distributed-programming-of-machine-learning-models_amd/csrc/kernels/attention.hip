@@ -762,8 +762,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
 }
 
 // ========================== backward: dK, dV ===============================
-template <typename T, int HD>
-__global__ __launch_bounds__(256, HD <= 64 ? 3 : 1) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+template <typename T, int HD, int OCC = (HD <= 64 ? 3 : 2)>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ Dv,
                                                             T* __restrict__ dqkv, const int* __restrict__ kv_len,
                                                             int B, int S, int H, float scale, uint64_t seed,
@@ -1596,9 +1596,20 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
                      (const T*)o.data_ptr(), (const T*)dout.data_ptr(), lse.data_ptr<float>(),
                      Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
   const int smem_kv = 2 * G::ROW_BYTES + 2 * G::TR_BYTES + 2 * 64 * 4;
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, HD>), dim3(B * H * nkt), dim3(256), smem_kv, st,
-                     (const T*)qkv.data_ptr(), (const T*)dout.data_ptr(), lse.data_ptr<float>(),
-                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+  // minimum waves per SIMD of the tiled dK/dV kernel (MIFT_ATTN_DKDV_OCC, read per call: A/B).  With the
+  // round-3 bound (HD <= 64 ? 3 : 1) hd 128 took 268 registers — one wave per SIMD, below the two its LDS
+  // allows; two: OPT-6.7B attention backward 629 -> 428 us (137 -> 201 TF/s), OPT-2.7B 184 -> 171 us;
+  // three spills (1084 / 230 us) (profiles/r4/bench_attn_dkdv_occupancy.txt)
+  const char* oe = getenv("MIFT_ATTN_DKDV_OCC");
+  const int occ = oe ? atoi(oe) : 0;
+  auto kv = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(B * H * nkt), dim3(256), smem_kv, st, (const T*)qkv.data_ptr(),
+                       (const T*)dout.data_ptr(), lse.data_ptr<float>(), Dv.data_ptr<float>(), (T*)dqkv.data_ptr(),
+                       kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+  };
+  if (occ == 2) kv(attn_bwd_dkdv_kernel<T, HD, 2>);
+  else if (occ == 3) kv(attn_bwd_dkdv_kernel<T, HD, 3>);
+  else kv(attn_bwd_dkdv_kernel<T, HD>);
 }
 
 }  // namespace
