@@ -492,7 +492,7 @@ def test_gemm_ext_masked():
     torch.testing.assert_close(out.float(), exp, atol=5e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19])
 @pytest.mark.parametrize("M,N,K", [(4096, 2560, 2560), (1000, 2304, 768), (8192, 768, 3072), (777, 1000, 320),
                                    (300, 520, 64), (64, 2304, 768), (64, 768, 3072), (7, 3072, 768)])
 def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):
@@ -516,14 +516,33 @@ def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):
     assert torch.equal(out, out2)
 
 
-@pytest.mark.parametrize("tile", [0, 3, 7, 8, 9])
+@pytest.mark.parametrize("kb32,kb64", [(16, 7), (17, 9), (18, 7), (19, 3)])
+@pytest.mark.parametrize("M,N,K", [(1000, 2304, 768), (8192, 768, 768), (300, 576, 64)])
+def test_gemm_half_depth_ring_bit_identical(kb32, kb64, M, N, K):
+    """The KB = 32 rings (4 / 3 half-depth stages, uneven LDS-DMA piece split over the waves) run the
+    same 32-deep MFMA k-steps in the same order as the KB = 64 tiles of equal shape: bit-identical
+    outputs with the full fused epilogue (no split-K at K <= 768)."""
+    C = _C()
+    torch.manual_seed(5)
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
+    b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    o32 = _gnt(C, a, b, bias, a2, b2, 1, None, res, 0.1, 5, True, 1.0, None, kb32, None, None, 0.0, 0)
+    o64 = _gnt(C, a, b, bias, a2, b2, 1, None, res, 0.1, 5, True, 1.0, None, kb64, None, None, 0.0, 0)
+    assert torch.equal(o32[0], o64[0]) and torch.equal(o32[1], o64[1])
+
+
+@pytest.mark.parametrize("tile", [0, 3, 7, 8, 9, 16, 17])
 @pytest.mark.parametrize("rows,p", [(8, 0.0), (8, 0.05), (24, 0.05)])
 def test_gemm_epilogue_projection_matches_lora_proj(tile, rows, p):
     """T = drop(out)·pwᵀ from the GEMM epilogue (per column tile partials in fp32 slabs, summed in
     order) == lora_proj over the stored output: same mask, fp32 sums, <= 16-bit rounding apart."""
     C = _C()
     torch.manual_seed(5)
-    M, K, N = 1000, 256, 768 if tile == 7 else 3072
+    M, K, N = 1000, 256, 768 if tile in (7, 16) else 3072
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
     bias = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)

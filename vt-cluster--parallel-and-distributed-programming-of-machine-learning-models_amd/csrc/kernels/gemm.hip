@@ -229,7 +229,24 @@ struct CTile {
   }
 };
 
-template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, bool SKM, int EPI = 0>
+// wait until at most N stages of LDS-DMA pieces are outstanding: PS_HI pieces per stage on waves
+// < NHI, PS_LO on the rest (the stage's pieces need not split evenly over the waves)
+template <int N, int PS_HI, int PS_LO, int NHI>
+MIFT_HD void wait_stages(int wave) {
+  if constexpr (PS_HI == PS_LO) {
+    wait_vmcnt<N * PS_HI>();
+  } else {
+    if (wave < NHI) wait_vmcnt<N * PS_HI>();
+    else wait_vmcnt<N * PS_LO>();
+  }
+}
+
+// KB: k-tile depth, 64 (128-B LDS rows, 16-B chunk c of row r at slot c ^ (r & 7)) or 32 (64-B rows:
+// four rows share a 256-B bank row, chunk c of row r at slot c ^ ((r >> 2) & 3) — the 16 rows of a
+// fragment read then cover the 16 slots of a bank row once, conflict-free as for KB = 64).  KB = 32
+// keeps the LDS of a 2-stage KB = 64 ring but holds 4 half-depth stages: three k-tiles in flight
+// instead of one for the K = 768 shapes whose main loop waits on LDS-DMA latency.
+template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, bool SKM, int EPI = 0, int KB = 64>
 __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                                 T* __restrict__ C, const T* __restrict__ A2,
                                                                 const T* __restrict__ B2, int M, int N, int K,
@@ -238,11 +255,18 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   constexpr int NT = NW * 64;
   constexpr int WM = BM / NWM, WN = BN / NWN;  // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;    // MFMA tiles per wave
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
+  static_assert(KB == 64 || (KB == 32 && NSTAGE > 0 && EPI == 0), "KB = 32: ring pipeline, plain GEMM only");
+  constexpr int KBY = KB * 2;       // bytes per LDS row
+  constexpr int RPP = 1024 / KBY;   // rows per 1-KiB LDS-DMA piece
+  constexpr int CPR = KB / 8;       // 16-B chunks per row
+  constexpr int A_BYTES = BM * KBY, B_BYTES = BN * KBY;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;  // 1-KiB LDS-DMA pieces per stage
-  static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "stage pieces must split evenly over waves");
-  constexpr int PER_STAGE = (A_INSTR + B_INSTR) / NW;  // vmcnt units per stage per wave
+  constexpr int A_INSTR = BM / RPP, B_INSTR = BN / RPP;  // 1-KiB LDS-DMA pieces per stage
+  constexpr bool EVEN = A_INSTR % NW == 0 && B_INSTR % NW == 0;
+  constexpr int P_ALL = A_INSTR + B_INSTR;
+  // vmcnt units per stage: PS_HI on waves < NHI, PS_LO on the others (all equal when EVEN)
+  constexpr int PS_LO = P_ALL / NW, NHI = P_ALL % NW, PS_HI = PS_LO + (NHI ? 1 : 0);
+  auto swz = [](int r) { return KB == 64 ? (r & 7) : ((r >> 2) & 3); };
   constexpr int NBUF = NSTAGE == 0 ? 2 : NSTAGE;       // NSTAGE 0 = phased schedule on 2 buffers
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (ep.sstep != nullptr) {
@@ -259,27 +283,43 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   int m0 = 0, n0 = 0;
 
-  // per-lane staging coordinates: lane -> (row-in-8 = lane>>3, phys chunk = lane&7)
-  const int srow = lane >> 3, spc = lane & 7;
+  // per-lane staging coordinates: lane -> (row in the piece, phys chunk) (lane-linear LDS-DMA destination)
+  const int srow = lane / CPR, spc = lane % CPR;
   auto stage = [&](int buf, int k0) {
     char* base = smem + buf * STAGE_BYTES;
+    if constexpr (EVEN) {
 #pragma unroll
-    for (int ii = 0; ii < A_INSTR / NW; ++ii) {
-      const int i = wave + ii * NW;
-      const int r = i * 8 + srow;
-      const int lc = spc ^ (r & 7);
-      const int gr = min(m0 + r, M - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)gr * lda + k0 + lc * 8), (void*)(base + i * 1024),
-                                       16, 0, 0);
-    }
+      for (int ii = 0; ii < A_INSTR / NW; ++ii) {
+        const int i = wave + ii * NW;
+        const int r = i * RPP + srow;
+        const int lc = spc ^ swz(r);
+        const int gr = min(m0 + r, M - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)gr * lda + k0 + lc * 8),
+                                         (void*)(base + i * 1024), 16, 0, 0);
+      }
 #pragma unroll
-    for (int ii = 0; ii < B_INSTR / NW; ++ii) {
-      const int i = wave + ii * NW;
-      const int r = i * 8 + srow;
-      const int lc = spc ^ (r & 7);
-      const int gr = min(n0 + r, N - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(B + (size_t)gr * ldb + k0 + lc * 8),
-                                       (void*)(base + A_BYTES + i * 1024), 16, 0, 0);
+      for (int ii = 0; ii < B_INSTR / NW; ++ii) {
+        const int i = wave + ii * NW;
+        const int r = i * RPP + srow;
+        const int lc = spc ^ swz(r);
+        const int gr = min(n0 + r, N - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(B + (size_t)gr * ldb + k0 + lc * 8),
+                                         (void*)(base + A_BYTES + i * 1024), 16, 0, 0);
+      }
+    } else {
+      // pieces 0 .. P_ALL-1 (A then B) round-robin over the waves (wave-uniform branches)
+#pragma unroll
+      for (int ii = 0; ii < PS_HI; ++ii) {
+        const int i = wave + ii * NW;
+        if (i < P_ALL) {
+          const bool isa = i < A_INSTR;
+          const int pi = isa ? i : i - A_INSTR;
+          const int r = pi * RPP + srow;
+          const int lc = spc ^ swz(r);
+          const T* src = isa ? A + (size_t)min(m0 + r, M - 1) * lda : B + (size_t)min(n0 + r, N - 1) * ldb;
+          __builtin_amdgcn_global_load_lds((const void*)(src + k0 + lc * 8), (void*)(base + i * 1024), 16, 0, 0);
+        }
+      }
     }
   };
 
@@ -297,18 +337,18 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     // prologue: NBUF-1 tiles in flight
 #pragma unroll
     for (int s = 0; s < NBUF - 1; ++s)
-      if (s < nk) stage(s, (kb + s) * BK);
+      if (s < nk) stage(s, (kb + s) * KB);
     for (int kt = 0; kt < nk; ++kt) {
-      // tile kt landed <=> at most (#tiles issued after kt) * PER_STAGE pieces outstanding:
+      // tile kt landed <=> at most (#tiles issued after kt) * (pieces per stage) outstanding:
       // min(NBUF - 2, nk - 1 - kt) tiles were issued after it (counted, never drained to 0 early)
       if constexpr (NBUF >= 4) {
         const int after = min(NBUF - 2, nk - 1 - kt);
-        if (after >= 2) wait_vmcnt<2 * PER_STAGE>();
-        else if (after == 1) wait_vmcnt<PER_STAGE>();
+        if (after >= 2) wait_stages<2, PS_HI, PS_LO, NHI>(wave);
+        else if (after == 1) wait_stages<1, PS_HI, PS_LO, NHI>(wave);
         else wait_vmcnt<0>();
-        static_assert(NBUF <= 4 && 2 * PER_STAGE < 64, "deeper rings need more wait cases");
+        static_assert(NBUF <= 4 && 2 * PS_HI < 64, "deeper rings need more wait cases");
       } else if constexpr (NBUF == 3) {
-        if (kt + 1 < nk) wait_vmcnt<PER_STAGE>();
+        if (kt + 1 < nk) wait_stages<1, PS_HI, PS_LO, NHI>(wave);
         else wait_vmcnt<0>();
       } else {
         wait_vmcnt<0>();
@@ -316,22 +356,22 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // everyone's pieces of kt landed; everyone done reading kt-1
       asm volatile("" ::: "memory");  // no LDS access may move above the barrier
-      if (kt + NBUF - 1 < nk) stage((kt + NBUF - 1) % NBUF, (kb + kt + NBUF - 1) * BK);
+      if (kt + NBUF - 1 < nk) stage((kt + NBUF - 1) % NBUF, (kb + kt + NBUF - 1) * KB);
       const char* As = smem + (kt % NBUF) * STAGE_BYTES;
       const char* Bs = As + A_BYTES;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < KB / 32; ++kk) {
         const int lc = kk * 4 + fq;
         frag_t<T> af[TM], bfv[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int r = wm * WM + i * 16 + fr;
-          af[i] = *reinterpret_cast<const frag_t<T>*>(As + r * ROWB + ((lc ^ (r & 7)) << 4));
+          af[i] = *reinterpret_cast<const frag_t<T>*>(As + r * KBY + ((lc ^ swz(r)) << 4));
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int r = wn * WN + j * 16 + fr;
-          bfv[j] = *reinterpret_cast<const frag_t<T>*>(Bs + r * ROWB + ((lc ^ (r & 7)) << 4));
+          bfv[j] = *reinterpret_cast<const frag_t<T>*>(Bs + r * KBY + ((lc ^ swz(r)) << 4));
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -795,7 +835,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     }
   };
 
-  const int nk_all = K / BK;
+  const int nk_all = K / KB;
   if constexpr (EPI == 1) {
     static_assert(NSTAGE == 0, "LM-head forward runs on the phased 256x256 tile");
     // one block per tile: a persistent loop over tiles (E stores draining under the next tile's main
@@ -1018,10 +1058,10 @@ __global__ __launch_bounds__(256) void proj_reduce_kernel(const float* __restric
   store8<T>(out + (size_t)m * 32 + c8, v);
 }
 
-template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE>
+template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, int KB = 64>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                  int K, const EpiArgs& ep, hipStream_t st) {
-  constexpr int STAGE_BYTES = (BM + BN) * ROWB;
+  constexpr int STAGE_BYTES = (BM + BN) * KB * 2;
   constexpr int EPI_BYTES = BM * CTile<BN>::CLD * 2;
   constexpr int RING = (NSTAGE == 0 ? 2 : NSTAGE) * STAGE_BYTES;
   constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
@@ -1030,8 +1070,8 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
   const int nblk = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   // the 256x256 tile has no register headroom for the split-K fixup (it would spill): DP only
   constexpr bool HAS_SK = BM * BN <= 256 * 128;
-  auto kern = gemm_nt_kernel<T, BM, BN, NWM, NWN, NSTAGE, false>;
-  auto kern_sk = gemm_nt_kernel<T, BM, BN, NWM, NWN, NSTAGE, HAS_SK>;
+  auto kern = gemm_nt_kernel<T, BM, BN, NWM, NWN, NSTAGE, false, 0, KB>;
+  auto kern_sk = gemm_nt_kernel<T, BM, BN, NWM, NWN, NSTAGE, HAS_SK, 0, KB>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -1043,7 +1083,6 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
   // chip: time ~ ceil(rem*S/G)/S tile-times instead of 1 (S chosen on that model + fixup cost)
   constexpr int BPC = (160 * 1024 / SMEM) < (2048 / NT) ? (160 * 1024 / SMEM) : (2048 / NT);
   const int G = num_cus() * (BPC > 0 ? BPC : 1);
-  const int nk = K / BK;
   const int rem = nblk % G;
   int sk_tiles = 0, S = 1;
   const int mode = sk_mode_env();
@@ -1051,7 +1090,7 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
     double best = 1.0;
     // chunks of >= 16 k-tiles: below that the fp32 partial round trip costs more than the
     // balanced wave saves (measured: K=768 GEMMs lost 2-4x with 3-k-tile chunks)
-    for (int s = 2; s <= 8 && nk / s >= 16; ++s) {
+    for (int s = 2; s <= 8 && K / s >= 1024; ++s) {
       const double cost = (double)((rem * s + G - 1) / G) / s + 0.03 * (s - 1);
       if (cost < best - 1e-9) { best = cost; S = s; }
     }
@@ -1485,6 +1524,11 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     case 7: launch_gemm<T, 128, 96, 2, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 8: launch_gemm<T, 256, 256, 2, 4, 0>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 9: launch_gemm<T, 128, 192, 2, 4, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    // half-depth (KB = 32) rings at the LDS of the KB = 64 two-stage tiles (A/B: tools/bench_kernels.py)
+    case 16: launch_gemm<T, 128, 96, 2, 2, 4, 32>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 17: launch_gemm<T, 128, 192, 2, 4, 4, 32>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 18: launch_gemm<T, 128, 96, 2, 2, 3, 32>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 19: launch_gemm<T, 128, 128, 2, 2, 4, 32>(a, b, c, a2, b2, M, N, K, ep, st); break;
     default: launch_gemm<T, 64, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
   }
 }
