@@ -69,6 +69,34 @@ def main():
         w = (torch.randn(N, Kd, device=dev) / Kd ** 0.5).to(dt)
         rec(f"gemm {name} {B}x{N}x{Kd}", lambda: K.gemm(xa, w))
         rec(f"gemm {name} tile4", lambda: K.gemm(xa, w, tile=4))
+    # epilogue-operand prefetch A/B (MIFT_SKINNY_PF, read per call) on the decode epilogues: bias (+gelu)
+    # for the LN-prologue GEMMs, bias + residual for c_proj / fc2 (K split 3)
+    res = torch.randn(B, d, device=dev).to(dt)
+    cases = []
+    for name, N, Kd, act in (("c_attn", 3 * d, d, 0), ("c_fc", 4 * d, d, 1)):
+        w = (torch.randn(N, Kd, device=dev) / Kd ** 0.5).to(dt)
+        bias = torch.randn(N, device=dev).to(dt)
+        cases.append((f"gemm_ln {name} +bias", lambda w=w, bias=bias, act=act: K.gemm_ln(x, lw, lb, 1e-5, w, bias, act=act)))
+    for name, Kd in (("attn.c_proj", d), ("mlp.c_proj", 4 * d)):
+        xa = torch.randn(B, Kd, device=dev).to(dt)
+        w = (torch.randn(d, Kd, device=dev) / Kd ** 0.5).to(dt)
+        bias = torch.randn(d, device=dev).to(dt)
+        cases.append((f"gemm {name} +bias+res", lambda xa=xa, w=w, bias=bias: K.gemm(xa, w, bias, residual=res)))
+    for name, fn in cases:
+        ts = {"0": [], "1": []}
+        outs = {}
+        for _ in range(3):
+            for pf in ("0", "1"):
+                os.environ["MIFT_SKINNY_PF"] = pf
+                ts[pf].append(timeit(fn))
+                outs[pf] = fn()
+        os.environ.pop("MIFT_SKINNY_PF")
+        same = torch.equal(outs["0"][0] if isinstance(outs["0"], tuple) else outs["0"],
+                           outs["1"][0] if isinstance(outs["1"], tuple) else outs["1"])
+        row = {"name": name, "pf0_us": round(min(ts["0"]) * 1e3, 2), "pf1_us": round(min(ts["1"]) * 1e3, 2),
+               "bit_identical": bool(same)}
+        print(json.dumps(row), flush=True)
+        rows.append(row)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(rows, f, indent=1)

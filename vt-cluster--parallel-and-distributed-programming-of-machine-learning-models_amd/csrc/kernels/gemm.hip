@@ -1147,7 +1147,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
                                                               const T* __restrict__ B2, int M, int N, int K, int lda,
                                                               int ldb, int ldc, EpiArgs ep, const T* __restrict__ lnw,
                                                               const T* __restrict__ lnb, float eps, int ksplit,
-                                                              float* __restrict__ kws, unsigned* __restrict__ kflags) {
+                                                              float* __restrict__ kws, unsigned* __restrict__ kflags,
+                                                              int pfe) {
   constexpr int NT = BN / 16;  // 16-column MFMA tiles per block
   constexpr int RLD = BN + 4;  // LDS row pitch (floats) of the partial tiles
   // dynamic LDS: the NW partial tiles, then (projection epilogue only) the rounded output tile
@@ -1175,6 +1176,22 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
 #pragma unroll
   for (int j = 0; j < NT; ++j) bp[j] = B + (size_t)min(n0 + j * 16 + fr, N - 1) * ldb + fq * 8;
   const int kper = K / 32 / ksplit, kb0 = sidx * kper, nks = kb0 + kper;
+  // epilogue operands of this thread's output chunk (one chunk per thread when 64 x BN / 8 <= threads)
+  // requested before the K loop: their latency hides under it instead of following the reduction
+  // barrier as one more dependent round trip (the decode step is a chain of such short kernels)
+  constexpr int CPR = BN / 8;  // 8-column chunks per row
+  constexpr bool PFE = 64 * CPR <= NW * 64;
+  short8 pf_bias = short8{0, 0, 0, 0, 0, 0, 0, 0}, pf_res = pf_bias;
+  const bool pf_b = PFE && pfe && ep.bias != nullptr && !ep.bias_f32;
+  const bool pf_r = PFE && pfe && ep.residual != nullptr;
+  if constexpr (PFE) {
+    const int row = tid / CPR, c8 = (tid % CPR) * 8;
+    if (tid < 64 * CPR && row < M && n0 + c8 < N) {
+      if (pf_b) pf_bias = *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.bias) + n0 + c8);
+      if (pf_r)
+        pf_res = *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.residual) + (size_t)row * ldc + n0 + c8);
+    }
+  }
   if constexpr (LNP) {
     // LayerNorm prologue (K <= 1024: at most KSM k-steps per wave).  All of the wave's fragments are
     // loaded first; the row statistics come from THOSE registers — per-lane partial sums over the
@@ -1296,11 +1313,13 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
       *reinterpret_cast<float4_*>(&red[w][i * 16 + fr][j * 16 + 4 * fq]) = acc[i][j];
   __syncthreads();
   const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
-  constexpr int CPR = BN / 8;  // 8-column chunks per row
-  auto finish = [&](int row, int c8, float* z) {
+  // pf: (row, c8) is this thread's prefetched chunk (ch == tid)
+  auto finish = [&](int row, int c8, float* z, bool pf) {
     const int gn = n0 + c8;
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (ep.bias != nullptr) {
+    if (pf && pf_b) {
+      unpack8<T>(pf_bias, bv);
+    } else if (ep.bias != nullptr) {
       if (ep.bias_f32) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) bv[e] = reinterpret_cast<const float*>(ep.bias)[gn + e];
@@ -1324,7 +1343,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
     }
     if (ep.residual != nullptr) {
       float rv[8];
-      load8<T>(reinterpret_cast<const T*>(ep.residual) + off, rv);
+      if (pf && pf_r) unpack8<T>(pf_res, rv);
+      else load8<T>(reinterpret_cast<const T*>(ep.residual) + off, rv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) z[e] += rv[e];
     }
@@ -1353,7 +1373,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
       for (int e = 0; e < 8; ++e) mift_st_sc1(dst + e, z[e]);
       continue;
     }
-    finish(row, c8, z);
+    finish(row, c8, z, PFE && ch == tid);
   }
   if (ksplit > 1) {
     __shared__ int klast;
@@ -1369,7 +1389,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
         z[0] += p0.x; z[1] += p0.y; z[2] += p0.z; z[3] += p0.w;
         z[4] += p1.x; z[5] += p1.y; z[6] += p1.z; z[7] += p1.w;
       }
-      finish(row, c8, z);
+      finish(row, c8, z, PFE && ch == tid);
     }
   }
   if (ep.pws == nullptr) return;  // block-uniform
@@ -1420,6 +1440,9 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
   }
   constexpr int RED = NW * 64 * (BN + 4) * 4, OT = 64 * (BN + 1) * 4;
   static_assert(RED + OT <= 160 * 1024, "LDS budget");
+  // epilogue-operand prefetch (MIFT_SKINNY_PF=0: off; read per call, A/B)
+  const char* pfs = getenv("MIFT_SKINNY_PF");
+  const int pfe = pfs ? atoi(pfs) : 1;
   const int smem = RED + (ep.pw != nullptr ? OT : 0);
   static bool attr = false;
   if (!attr) {
@@ -1436,14 +1459,14 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
       hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, true>), dim3(nb), dim3(NW * 64), smem, st,
                          (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
                          (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, lnw, lnb, eps, 1,
-                         (float*)nullptr, (unsigned*)nullptr);
+                         (float*)nullptr, (unsigned*)nullptr, pfe);
     else
       TORCH_CHECK(false, "gemm_skinny: LN prologue needs the 16-column 8-wave form");
   } else
     hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, false>), dim3(nb * ksplit), dim3(NW * 64), smem, st,
                        (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
                        (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, (const T*)nullptr,
-                       (const T*)nullptr, 0.f, ksplit, kws, kflags);
+                       (const T*)nullptr, 0.f, ksplit, kws, kflags, pfe);
   if (ep.pw != nullptr)
     hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
                        (const float*)epx.pws, nb, M, PW, ep.palpha, (T*)ep.pout);
