@@ -188,7 +188,8 @@ def main():
         {"gemm": bench_gemm, "ln": bench_ln, "dgpt": bench_dgpt, "epi": bench_epi_ab,
          "opt": lambda r: bench_gemm(r, OPT_SHAPES, torch.float16),
          "optm": lambda r: bench_dgpt(r, opt_m_cases(), torch.float16),
-         "optm_small": lambda r: bench_dgpt(r, opt_m_cases((2048, 4096)), torch.float16)}[k](results)
+         "optm_small": lambda r: bench_dgpt(r, opt_m_cases((2048, 4096)), torch.float16),
+         "optm_pp": lambda r: bench_dgpt(r, opt_m_cases((2048, 6144)), torch.float16)}[k](results)
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
         with open(a.json, "w") as f:

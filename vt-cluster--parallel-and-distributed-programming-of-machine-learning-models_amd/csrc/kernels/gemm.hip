@@ -1524,7 +1524,12 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     //    256x256 tiles with a gelu/pre-activation epilogue tile 8 ran 10-20 % slower end to end.
     const long n256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+    const long t96 = (long)((M + 127) / 128) * ((N + 95) / 96);
     if ((K >= 1024 && n256 >= 128) || n256 >= 2048) tile = 8;
+    // one chip-wave of 128x96 tiles (1-2 per CU): the OPT micro-batch-4 shapes (M = 2048, N = 2560)
+    // ran 20-30 % faster than on the 128x256 split-K / 128x128 tiles (fc2 fwd 167 -> 122 us, qkv dgrad
+    // 134 -> 94, out proj 50 -> 40; profiles/r4/bench_tiles_opt_pp_microbatch.json)
+    else if (t96 >= num_cus() && t96 <= 2L * num_cus()) tile = 7;
     else if (K >= 4096 && t128 >= 128) tile = 6;
     else if (N % 192 == 0 && (long)((M + 127) / 128) * (N / 192) >= 2L * num_cus()) tile = 9;
     else if (t128 >= 64) {
@@ -1552,6 +1557,10 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     case 17: launch_gemm<T, 128, 192, 2, 4, 4, 32>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 18: launch_gemm<T, 128, 96, 2, 2, 3, 32>(a, b, c, a2, b2, M, N, K, ep, st); break;
     case 19: launch_gemm<T, 128, 128, 2, 2, 4, 32>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    // 8-wave forms of the 128-row tiles (4x2 waves, wave tiles 32x48 / 32x64): twice the waves per CU
+    // at the same LDS (A/B: tools/bench_kernels.py)
+    case 20: launch_gemm<T, 128, 96, 4, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
+    case 21: launch_gemm<T, 128, 128, 4, 2, 2>(a, b, c, a2, b2, M, N, K, ep, st); break;
     default: launch_gemm<T, 64, 64, 2, 2, 3>(a, b, c, a2, b2, M, N, K, ep, st); break;
   }
 }
