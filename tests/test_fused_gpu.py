@@ -218,3 +218,38 @@ def test_fused_backward_notifies_dp_reducer_per_layer(monkeypatch):
         assert any(kind == "gemm" for kind, _ in events[last_of[l] + 1:]), (l, events)
     # and the arena grads are the real ones (non-zero)
     assert arena.grad.abs().sum().item() > 0
+
+
+def test_ln_backward_handoff_fires_and_matches_separate_passes(monkeypatch):
+    """GradHandoff: at D = 768 every LN backward that feeds a LoRA linear's residual-dropout backward runs
+    them as one pass (ln_bwd_mask_proj: the MLP's LN for attn.c_proj in every block, the next block's
+    ln_1 for mlp.c_proj), and the LoRA gradients match the separate LN-bwd + mask_proj passes."""
+    from mift.ops import kernels as K
+    cfg = GPT2Config(vocab_size=1000, n_positions=128, n_embd=768, n_layer=3, n_head=12, n_inner=3072,
+                     embd_pdrop=0.1, attn_pdrop=0.1, resid_pdrop=0.1)
+    m = GPT2LMHeadModel(cfg, dtype=torch.bfloat16, device="cuda").init_weights(5)
+    L.inject(m, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["c_attn", "c_proj"]))
+    for _, p in L.lora_parameters(m):
+        with torch.no_grad():
+            p.normal_(0, 0.05)
+    m.train()
+    ids = torch.randint(0, cfg.vocab_size, (4, 128), device="cuda")
+    calls = []
+    orig = K.ln_bwd_mask_proj
+    monkeypatch.setattr(K, "ln_bwd_mask_proj", lambda *a, **k: calls.append(1) or orig(*a, **k))
+
+    def grads(on):
+        monkeypatch.setenv("MIFT_LN_MASK_PROJ", "1" if on else "0")
+        for _, p in L.lora_parameters(m):
+            p.grad = None
+        m.micro_step = 3
+        m(input_ids=ids, labels=ids, reduction="sum")["loss"].backward()
+        return [p.grad.float().clone() for _, p in L.lora_parameters(m)]
+
+    g1 = grads(True)
+    assert len(calls) == 2 * cfg.n_layer - 1, len(calls)
+    g0 = grads(False)
+    assert len(calls) == 2 * cfg.n_layer - 1
+    for a, b in zip(g1, g0):
+        rel = (a - b).norm() / (b.norm() + 1e-6)
+        assert rel < 2e-2, rel

@@ -661,3 +661,40 @@ def test_gemm_ln_prologue(M, N, K, act):
     z = ref_a @ w.float().t() + bias.float()
     ref_y = {0: z, 1: torch.nn.functional.gelu(z, approximate="tanh"), 2: torch.relu(z)}[act]
     torch.testing.assert_close(y.float(), ref_y, atol=6e-2, rtol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,rank,p,dres,wf32", [(768, 8, 0.1, True, False), (768, 24, 0.0, True, False),
+                                               (1024, 8, 0.1, False, True), (768, 8, 0.1, True, True)])
+def test_ln_bwd_mask_proj_matches_separate_passes(D, rank, p, dres, wf32):
+    """rowproj MODE 3 (LN backward + residual-dropout backward + dT projection in one pass) against
+    layer_norm_bwd followed by mask_proj, and against the fp32 reference of the three ops."""
+    from mift.ops import kernels as K
+    torch.manual_seed(3)
+    M, dt = 1000, torch.bfloat16
+    x = torch.randn(M, D, device="cuda").to(dt)
+    dy = torch.randn(M, D, device="cuda").to(dt)
+    w = (1 + 0.1 * torch.randn(D, device="cuda")).to(torch.float32 if wf32 else dt)
+    b = torch.zeros(D, device="cuda", dtype=w.dtype)
+    _, mean, rstd = K.layer_norm_fwd(x, w, b, 1e-5)
+    gr = torch.randn(M, D, device="cuda").to(dt) if dres else None
+    pw = torch.zeros(32, D, device="cuda", dtype=dt)
+    pw[:rank] = (torch.randn(rank, D, device="cuda") / D ** 0.5).to(dt)
+    dh, y, pr = K.ln_bwd_mask_proj(dy, x, w, mean, rstd, gr, p, 77, pw, rank, 0.5)
+    dh0 = K.layer_norm_bwd(dy, x, w, mean, rstd, dres=gr)[0]
+    y0, pr0 = K.mask_proj(dh0, p, 77, pw, rank, 0.5)
+    # the row sums run in another order: dh within one 16-bit rounding of the separate pass
+    torch.testing.assert_close(dh.float(), dh0.float(), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(y.float(), y0.float(), atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(pr.float(), pr0.float(), atol=3e-2, rtol=2e-2)
+    if p == 0:
+        assert y.data_ptr() == dh.data_ptr()
+    # fp32 reference of LN backward + residual
+    xf = x.float().requires_grad_(True)
+    yf = torch.nn.functional.layer_norm(xf, (D,), w.float(), b.float(), 1e-5)
+    yf.backward(dy.float())
+    ref = xf.grad + (gr.float() if dres else 0)
+    torch.testing.assert_close(dh.float(), ref, atol=3e-2, rtol=2e-2)
+    keep = (y0 != 0) | (dh0 == 0)
+    torch.testing.assert_close((pr.float()[:, :rank]), (0.5 * y.float() @ pw.float()[:rank].t()), atol=3e-2, rtol=2e-2)
+    assert keep.all() if p == 0 else True

@@ -237,7 +237,11 @@ __global__ __launch_bounds__(256) void mask_proj_kernel(const T* __restrict__ x,
 // elements zeroed (1/(1-p) folded into alpha by the host for LN), fp32 accumulation.
 // MODE: 0 = residual-dropout backward (y = keep·x/(1-p) stored and projected), 1 = LN (y = LN(x)
 // stored, LoRA-input dropout on the projection), 2 = plain LoRA projection (lora_proj semantics:
-// T = alpha·drop(x)·Wᵀ, nothing stored; replaces lora_proj's 16-row blocks at these widths).
+// T = alpha·drop(x)·Wᵀ, nothing stored; replaces lora_proj's 16-row blocks at these widths),
+// 3 = LN backward feeding a residual-dropout backward: x = dY of the LN, xin = its input, lw its
+// weight, mean_out / rstd_out its saved statistics (read); dh = LN-bwd(dY) + dres is stored (the
+// residual-stream gradient), then MODE 0 on the rounded dh (the upstream LoRA linear's dropout and
+// dT = s·y·Bᵀ) — the separate MODE 0 pass re-read dh (one launch and 12.6 MB per site at distilgpt2).
 template <typename T, typename W, int NK, int NTI, int MODE>
 __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__ x, const W* __restrict__ lw,
                                                            const W* __restrict__ lb, T* __restrict__ y,
@@ -245,7 +249,9 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
                                                            const T* __restrict__ pw, T* __restrict__ pout, int M,
                                                            float eps, float alpha, uint64_t seed,
                                                            const int64_t* __restrict__ sstep, uint32_t thr,
-                                                           float inv_keep, int wrows, int write_y) {
+                                                           float inv_keep, int wrows, int write_y,
+                                                           const T* __restrict__ xin, const T* __restrict__ dres,
+                                                           T* __restrict__ dh) {
   using frag = typename std::conditional<std::is_same<T, bf16>::value, bf16x8, fp16x8>::type;
   constexpr int D = NK * 32;
   constexpr int NKW = NK / 4;  // k-steps per wave
@@ -313,6 +319,74 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
       mean_out[m0 + fr] = mean;
       rstd_out[m0 + fr] = rstd;
     }
+  } else if constexpr (MODE == 3) {
+    const float mean = mean_out[row], rstd = rstd_out[row];
+    short8 hv[NKW], rv[NKW];
+    const T* hr = xin + (size_t)row * D + c00;
+#pragma unroll
+    for (int s = 0; s < NKW; ++s) {
+      hv[s] = *reinterpret_cast<const short8*>(hr + s * 32);
+      rv[s] = dres != nullptr ? *reinterpret_cast<const short8*>(dres + (size_t)row * D + c00 + s * 32)
+                              : short8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int s = 0; s < NKW; ++s) {
+      float dv[8], xf[8], wv[8];
+      unpack8<T>(xv[s], dv);
+      unpack8<T>(hv[s], xf);
+      load8<W>(lw + c00 + s * 32, wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gg = dv[e] * wv[e];
+        sg += gg;
+        sgx += gg * ((xf[e] - mean) * rstd);
+      }
+    }
+    {  // both row sums in one LDS exchange (one barrier pair instead of two)
+      __shared__ float red2[4][16][2];
+      sg += __shfl_xor(sg, 16, 64);
+      sg += __shfl_xor(sg, 32, 64);
+      sgx += __shfl_xor(sgx, 16, 64);
+      sgx += __shfl_xor(sgx, 32, 64);
+      if (g == 0) {
+        red2[wave][fr][0] = sg;
+        red2[wave][fr][1] = sgx;
+      }
+      __syncthreads();
+      sg = (red2[0][fr][0] + red2[1][fr][0] + red2[2][fr][0] + red2[3][fr][0]) * (1.f / D);
+      sgx = (red2[0][fr][1] + red2[1][fr][1] + red2[2][fr][1] + red2[3][fr][1]) * (1.f / D);
+    }
+    T* dhr = dh + (size_t)row * D + c00;
+#pragma unroll
+    for (int s = 0; s < NKW; ++s) {
+      float dv[8], xf[8], wv[8], r[8], o[8];
+      unpack8<T>(xv[s], dv);
+      unpack8<T>(hv[s], xf);
+      unpack8<T>(rv[s], r);
+      load8<W>(lw + c00 + s * 32, wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = rstd * (dv[e] * wv[e] - sg - (xf[e] - mean) * rstd * sgx) + r[e];
+      short8 hq;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { T t = (T)o[e]; short h; __builtin_memcpy(&h, &t, 2); hq[e] = h; }
+      if (live) *reinterpret_cast<short8*>(dhr + s * 32) = hq;
+      if (thr != 0) {
+        bool kp[8];
+        mift_keep8(seed, (uint64_t)row * D + c00 + s * 32, thr, kp);
+        float v[8];
+        unpack8<T>(hq, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          T t = (T)(kp[e] ? v[e] * inv_keep : 0.f);
+          short h;
+          __builtin_memcpy(&h, &t, 2);
+          hq[e] = h;
+        }
+        if (live) *reinterpret_cast<short8*>(yr + s * 32) = hq;
+      }
+      xv[s] = hq;
+    }
   } else if (MODE == 0 && thr != 0) {  // residual-dropout backward: y = keep ? x/(1-p) : 0, stored and projected
 #pragma unroll
     for (int s = 0; s < NKW; ++s) {
@@ -334,7 +408,7 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
   }
   // projection partial over this wave's k-steps: acc[j] = y[16 rows] · pw[16j .. 16j+15]^T (rows
   // >= wrows of pw are zero: not read)
-  const bool mask_in = MODE != 0 && thr != 0;  // LoRA-input dropout (1/(1-p) folded into alpha by the host)
+  const bool mask_in = (MODE == 1 || MODE == 2) && thr != 0;  // LoRA-input dropout (1/(1-p) folded into alpha)
   const uint32_t hm0 = mift_hmix(seed, 0);
   const bool hz = (uint64_t)M * D < (1ull << 33);
   float4_ acc[NTI];
@@ -461,7 +535,8 @@ std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::
         hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(),
                            (const Wt*)w.data_ptr(), (const Wt*)b.data_ptr(), (T*)y.data_ptr(), mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, (float)eps,
-                           (float)alpha * inv, (uint64_t)seed, mift_seed_step(), thr, inv, (int)rank, 1);
+                           (float)alpha * inv, (uint64_t)seed, mift_seed_step(), thr, inv, (int)rank, 1,
+                           (const T*)nullptr, (const T*)nullptr, (T*)nullptr);
       });
     };
     if (x.scalar_type() == at::kBFloat16) {
@@ -519,7 +594,8 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
         hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
                            (const T*)nullptr, (T*)y.data_ptr(), (float*)nullptr, (float*)nullptr,
                            (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, 0.f, (float)alpha, (uint64_t)seed,
-                           mift_seed_step(), thr, inv, (int)rank, thr != 0 ? 1 : 0);
+                           mift_seed_step(), thr, inv, (int)rank, thr != 0 ? 1 : 0, (const T*)nullptr,
+                           (const T*)nullptr, (T*)nullptr);
       });
     };
     if (x.scalar_type() == at::kBFloat16) go2(bf16{});
@@ -541,6 +617,57 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
   if (x.scalar_type() == at::kBFloat16) go(bf16{});
   else go(fp16{});
   return {y, pout};
+}
+
+// (dh, y, proj[M,32]): dh = LN-bwd(dy; x, w, mean, rstd) + dres, y = keep⊙dh/(1-p) (dh itself when
+// p == 0), proj = alpha·y·pw^T — layer_norm_bwd followed by mask_proj in one pass (MFMA form only:
+// D in {768, 1024}; the caller checks mift_ln_bwd_mask_proj_ok)
+bool mift_ln_bwd_mask_proj_ok(int64_t D) { return rowproj_mfma_ok((int)D); }
+
+std::vector<at::Tensor> mift_ln_bwd_mask_proj(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                              const at::Tensor& mean, const at::Tensor& rstd,
+                                              const c10::optional<at::Tensor>& dres, double p, int64_t seed,
+                                              const at::Tensor& pw, int64_t rank, double alpha) {
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.dim() == 2, "ln_bwd_mask_proj: contiguous 2-D GPU dy");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf, "ln_bwd_mask_proj: bf16/fp16");
+  const int D = dy.size(1);
+  const int M = dy.size(0);
+  TORCH_CHECK(rowproj_mfma_ok(D), "ln_bwd_mask_proj: D in {768, 1024}");
+  TORCH_CHECK(x.is_contiguous() && x.sizes() == dy.sizes() && x.scalar_type() == dy.scalar_type(), "ln_bwd_mask_proj: x");
+  TORCH_CHECK(!dres || (dres->is_contiguous() && dres->sizes() == dy.sizes() && dres->scalar_type() == dy.scalar_type()),
+              "ln_bwd_mask_proj: dres");
+  TORCH_CHECK(w.numel() == D && (w.scalar_type() == dy.scalar_type() || w.scalar_type() == at::kFloat), "ln_bwd_mask_proj: w");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && rstd.scalar_type() == at::kFloat && mean.numel() == M &&
+              rstd.numel() == M, "ln_bwd_mask_proj: mean / rstd");
+  check_pw(dy, pw, D, rank);
+  const uint32_t thr = mift_thr16(p);
+  auto dh = at::empty_like(dy);
+  at::Tensor y = thr != 0 ? at::empty_like(dy) : dh;
+  auto pout = at::empty({M, 32}, dy.options());
+  if (M == 0) return {dh, y, pout};
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  const float inv = p > 0 ? mift_inv_keep(p) : 1.f;
+  const bool wf32 = w.scalar_type() == at::kFloat;
+  auto go = [&](auto tt, auto wt) {
+    using T = decltype(tt);
+    using Wt = decltype(wt);
+    by_nk(D, [&](auto nk) {
+      constexpr int NK = decltype(nk)::value;
+      auto kern = rank <= 16 ? rowproj_mfma_kernel<T, Wt, NK, 1, 3> : rowproj_mfma_kernel<T, Wt, NK, 2, 3>;
+      hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)dy.data_ptr(), (const Wt*)w.data_ptr(),
+                         (const Wt*)nullptr, (T*)y.data_ptr(), const_cast<float*>(mean.data_ptr<float>()),
+                         const_cast<float*>(rstd.data_ptr<float>()), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M,
+                         0.f, (float)alpha, (uint64_t)seed, mift_seed_step(), thr, inv, (int)rank, thr != 0 ? 1 : 0,
+                         (const T*)x.data_ptr(), dres ? (const T*)dres->data_ptr() : (const T*)nullptr,
+                         (T*)dh.data_ptr());
+    });
+  };
+  if (dy.scalar_type() == at::kBFloat16) {
+    if (wf32) go(bf16{}, 0.f); else go(bf16{}, bf16{});
+  } else {
+    if (wf32) go(fp16{}, 0.f); else go(fp16{}, fp16{});
+  }
+  return {dh, y, pout};
 }
 
 // lora_proj on the 4-wave 16-row MFMA form (MODE 2) for contiguous x at K in {768, 1024, 2304}:
@@ -567,7 +694,7 @@ bool mift_rowproj_lora_proj(const at::Tensor& x, const at::Tensor& w, at::Tensor
       hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
                          (const T*)nullptr, (T*)nullptr, (float*)nullptr, (float*)nullptr, (const T*)w.data_ptr(),
                          (T*)out.data_ptr(), M, 0.f, (float)alpha * ik, (uint64_t)seed, mift_seed_step(), thr, ik,
-                         (int)rows, 0);
+                         (int)rows, 0, (const T*)nullptr, (const T*)nullptr, (T*)nullptr);
     });
   };
   if (x.scalar_type() == at::kBFloat16) go(bf16{});

@@ -47,6 +47,11 @@ void mift_pack_lora_all(const at::Tensor& arena, const at::Tensor& table, const 
 std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
                                                  double eps, const at::Tensor& pw, int64_t rank, double alpha,
                                                  double p, int64_t seed);
+bool mift_ln_bwd_mask_proj_ok(int64_t D);
+std::vector<at::Tensor> mift_ln_bwd_mask_proj(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                              const at::Tensor& mean, const at::Tensor& rstd,
+                                              const c10::optional<at::Tensor>& dres, double p, int64_t seed,
+                                              const at::Tensor& pw, int64_t rank, double alpha);
 std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t seed, const at::Tensor& pw,
                                        int64_t rank, double alpha);
 
@@ -109,6 +114,8 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
   m.def("lora_proj", &mift_lora_proj, "out[M,32] = alpha*drop(x)@w^T (tall-skinny MFMA)"); \
   m.def("layer_norm_fwd_proj", &mift_layer_norm_fwd_proj, "LN fwd + alpha*drop(y)@pw^T -> (y, mean, rstd, proj)"); \
   m.def("mask_proj", &mift_mask_proj, "y = dropout(x) (p>0), proj = alpha*y@pw^T -> (y, proj)"); \
+  m.def("ln_bwd_mask_proj_ok", &mift_ln_bwd_mask_proj_ok, "ln_bwd_mask_proj applies at this width");            \
+  m.def("ln_bwd_mask_proj", &mift_ln_bwd_mask_proj, "dh = LN-bwd + dres, y = dropout-bwd(dh), proj = alpha*y@pw^T"); \
   m.def("lora_wgrad", &mift_lora_wgrad, "out[P,32] += drop(x)^T @ y (tr_b16 split-M MFMA); arena modes"); \
   m.def("lora_wgrad_group", &mift_lora_wgrad_group, "grouped LoRA weight grads (<= 16 problems, one launch)"); \
   m.def("pack_lora_all", &mift_pack_lora_all, "pack every adapter's 16-bit operands from the fp32 arena"); \

@@ -138,10 +138,12 @@ class GPT2Block(nn.Module):
         else:
             o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5, dropout_p=cfg.attn_pdrop if training else 0.0,
                                  seed=seeds["attn"], kv_len=kv_len)
+        # the MLP's LN backward also runs c_proj's residual-dropout backward + dT (one row pass)
+        hand = F.GradHandoff() if training and torch.is_grad_enabled() else None
         h = F.linear_residual(o, h, self.attn.c_proj, cfg.resid_pdrop, seeds["attn_out"], seeds["lora_proj"],
-                              training, link=link)
+                              training, link=link, handoff=hand)
         return F.mlp(h, self.ln_2, self.mlp.c_fc, self.mlp.c_proj, act=1, p=cfg.resid_pdrop, seed=seeds["mlp_out"],
-                     seed_l1=0, seed_l2=seeds["lora_mlp"], training=training)
+                     seed_l1=0, seed_l2=seeds["lora_mlp"], training=training, handoff=hand)
 
 
 class GPT2LMHeadModel(CausalLMBase):

@@ -170,10 +170,12 @@ class OPTDecoderLayer(nn.Module):
             o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5,
                                  dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"],
                                  kv_len=kv_len)
+        # the MLP's LN backward also runs out_proj's residual-dropout backward + dT (one row pass)
+        hand = F.GradHandoff() if training and torch.is_grad_enabled() else None
         h = F.linear_residual(o, h, at.out_proj, cfg.dropout, seeds["attn_out"], seeds["lora_proj"], training,
-                              link=link)
+                              link=link, handoff=hand)
         return F.mlp(h, self.final_layer_norm, self.fc1, self.fc2, act=2, p=cfg.dropout, seed=seeds["mlp_out"],
-                     seed_l1=seeds["lora_fc1"], seed_l2=seeds["lora_fc2"], training=training)
+                     seed_l1=seeds["lora_fc1"], seed_l2=seeds["lora_fc2"], training=training, handoff=hand)
 
 
 class OPTLearnedPositionalEmbedding(Embedding):

@@ -343,6 +343,57 @@ class ResidualLink:
         self.g = None
 
 
+class GradHandoff:
+    """An LN backward hands its output straight to the residual-dropout backward of the LoRA linear
+    that produced the LN's input, in one row pass (K.ln_bwd_mask_proj, rowproj.hip MODE 3).
+
+    The consumer (``linear_residual`` / ``mlp``: h' = h + dropout(lin(..)), LoRA on lin) registers its
+    dropout (p, seed) and adapter in forward; the producer (the LN backward of the NEXT op in forward
+    order, whose LN reads h') computes dh, y = dropout-bwd(dh) and dT0 = s·y·Bᵀ together and leaves
+    (dh, y, dT0) here; the consumer's backward takes them when the gradient it receives IS that dh
+    (same storage), else it runs its own mask_proj.  MIFT_LN_MASK_PROJ=0 turns the fusion off."""
+    __slots__ = ("p", "seed", "lo", "out")
+
+    def __init__(self):
+        self.p, self.seed, self.lo, self.out = None, 0, None, None
+
+    def register(self, p, seed, lo):
+        self.p, self.seed, self.lo, self.out = p, seed, lo, None
+
+    def ready(self, D):
+        return (self.lo is not None and os.environ.get("MIFT_LN_MASK_PROJ", "1") != "0"
+                and K.ln_bwd_mask_proj_ok(D))
+
+    def ln_bwd(self, da, x2, ln_w, mean, rstd, dres):
+        """LN backward (+ dres); with a registered consumer also its mask_proj, kept for it."""
+        if not self.ready(x2.shape[-1]):
+            return K.layer_norm_bwd(da, x2, ln_w, mean, rstd, dres=dres)[0]
+        lo = self.lo
+        dh, y, dT0 = K.ln_bwd_mask_proj(da, x2, ln_w, mean, rstd, dres, self.p, self.seed, lo.B32t, lo.rows,
+                                        lo.dt_alpha)
+        self.out = (dh, y, dT0)
+        return dh
+
+    def take(self, g2):
+        """(y, dT0) computed for gradient g2 by the LN backward, or None."""
+        out, self.out = self.out, None
+        if out is None or out[0].data_ptr() != g2.data_ptr() or out[0].shape != g2.shape:
+            return None
+        return out[1], out[2]
+
+
+def _ln_bwd(hand, da, x2, ln_w, mean, rstd, dres):
+    if hand is not None:
+        return hand.ln_bwd(da, x2, ln_w, mean, rstd, dres)
+    return K.layer_norm_bwd(da, x2, ln_w, mean, rstd, dres=dres)[0]
+
+
+def _mask_proj_in(hand, g2, p, seed, lo):
+    """The consumer side of GradHandoff: the LN backward's (gz, dT0) for g2, or a mask_proj pass."""
+    got = hand.take(g2) if hand is not None else None
+    return got if got is not None else _mask_proj(g2, p, seed, lo)
+
+
 class LnLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, ln_w, ln_b, lin, eps, lora_seed, training, link, *lparams):
@@ -358,6 +409,7 @@ class LnLinear(torch.autograd.Function):
         ctx.save_for_backward(x2, a, mean, rstd, ln_w, T32)
         ctx.lin, ctx.lo, ctx.seed, ctx.training, ctx.shp, ctx.nl = lin, lo, lora_seed, training, shp, len(lparams)
         ctx.link = link
+        ctx.hand = getattr(x, "_mift_hand", None)  # the upstream mlp's dropout-bwd rides on this LN backward
         return y.view(*shp[:-1], y.shape[-1])
 
     @staticmethod
@@ -374,7 +426,7 @@ class LnLinear(torch.autograd.Function):
             # e.g. the first block, fed by the frozen embedding: no dX -> no dgrad GEMM, no LN backward
             return (None, None, None, None, None, None, None, None, *lg)
         da = _dgrad(gy, lin, lo, dT32, ctx.seed, ctx.training)
-        dx, _, _, _ = K.layer_norm_bwd(da, x2, ln_w, mean, rstd, dres=None if gres is None else _flat(gres.contiguous()))
+        dx = _ln_bwd(ctx.hand, da, x2, ln_w, mean, rstd, None if gres is None else _flat(gres.contiguous()))
         return (dx.view(ctx.shp), None, None, None, None, None, None, None, *lg)
 
 
@@ -400,7 +452,7 @@ def ln_linear(x, ln, lin, lora_seed=0, training=True, link=None):
 # ---------------------------------------------------------------------------
 class LinearResidual(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, h, lin, p, seed, lora_seed, training, link, *lparams):
+    def forward(ctx, x, h, lin, p, seed, lora_seed, training, link, hand, *lparams):
         shp = h.shape
         x2 = _flat(x.contiguous())
         h2 = _flat(h.contiguous())
@@ -411,6 +463,9 @@ class LinearResidual(torch.autograd.Function):
         ctx.save_for_backward(x2, T32)
         ctx.lin, ctx.lo, ctx.p, ctx.seed, ctx.lseed = lin, lo, pp, seed, lora_seed
         ctx.training, ctx.xshp, ctx.nl, ctx.link = training, x.shape, len(lparams), link
+        ctx.hand = hand
+        if hand is not None:
+            hand.register(pp, seed, lo)
         return y.view(shp)
 
     @staticmethod
@@ -419,7 +474,7 @@ class LinearResidual(torch.autograd.Function):
         lin, lo = ctx.lin, ctx.lo
         gh2 = _flat(gh.contiguous())
         if lo is not None:  # residual-dropout backward and dT = s·gz·B in one row pass
-            gz, dT0 = _mask_proj(gh2, ctx.p, ctx.seed, lo)
+            gz, dT0 = _mask_proj_in(ctx.hand, gh2, ctx.p, ctx.seed, lo)
             lg, dT32 = lo.backward(gz, x2, T32, ctx.lseed, ctx.training, dT32=dT0)
         else:
             gz = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
@@ -428,11 +483,13 @@ class LinearResidual(torch.autograd.Function):
         gres = gh
         if ctx.link is not None and ctx.needs_input_grad[1]:
             ctx.link.g, gres = gh, None  # delivered through the linked ln_linear's LN backward
-        return (dx.view(ctx.xshp), gres, None, None, None, None, None, None, *lg)
+        return (dx.view(ctx.xshp), gres, None, None, None, None, None, None, None, *lg)
 
 
-def linear_residual(x, h, lin, p, seed, lora_seed=0, training=True, link=None):
-    return LinearResidual.apply(x, h, lin, p, seed, lora_seed, training, link, *lin.lora_params())
+def linear_residual(x, h, lin, p, seed, lora_seed=0, training=True, link=None, handoff=None):
+    """h + dropout(lin(x)); ``handoff`` (GradHandoff): the following LN backward also runs this
+    op's residual-dropout backward + dT projection."""
+    return LinearResidual.apply(x, h, lin, p, seed, lora_seed, training, link, handoff, *lin.lora_params())
 
 
 # ---------------------------------------------------------------------------
@@ -440,7 +497,8 @@ class MLP(torch.autograd.Function):
     """h' = h + dropout(fc2(act(fc1(LN(h)))))."""
 
     @staticmethod
-    def forward(ctx, h, ln_w, ln_b, fc1, fc2, eps, act, p, seed, seed_l1, seed_l2, training, n1, *lparams):
+    def forward(ctx, h, ln_w, ln_b, fc1, fc2, eps, act, p, seed, seed_l1, seed_l2, training, n1, hand_out, hand_in,
+                *lparams):
         shp = h.shape
         h2 = _flat(h.contiguous())
         lo1 = fc1.lora_ops(h.dtype) if n1 else None
@@ -468,6 +526,9 @@ class MLP(torch.autograd.Function):
         ctx.fc1, ctx.fc2, ctx.lo1, ctx.lo2 = fc1, fc2, lo1, lo2
         ctx.act, ctx.p, ctx.seed, ctx.sl1, ctx.sl2, ctx.training, ctx.shp = act, pp, seed, seed_l1, seed_l2, training, shp
         ctx.n1, ctx.n2 = n1, len(lparams) - n1
+        ctx.hand_out, ctx.hand_in = hand_out, hand_in
+        if hand_in is not None:
+            hand_in.register(pp, seed, lo2)
         return out.view(shp)
 
     @staticmethod
@@ -478,7 +539,7 @@ class MLP(torch.autograd.Function):
         lg1, lg2 = _nones(ctx.n1), _nones(ctx.n2)
         dT1 = dT2 = None
         if lo2 is not None:  # residual-dropout backward fused with dT2 = s·gm·B2
-            gm, dT0 = _mask_proj(gh2, ctx.p, ctx.seed, lo2)
+            gm, dT0 = _mask_proj_in(ctx.hand_in, gh2, ctx.p, ctx.seed, lo2)
             lg2, dT2 = lo2.backward(gm, f, T2, ctx.sl2, ctx.training, dT32=dT0)
         else:
             gm = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
@@ -487,11 +548,14 @@ class MLP(torch.autograd.Function):
         if lo1 is not None:
             lg1, dT1 = lo1.backward(dz, a, T1, ctx.sl1, ctx.training)
         da = _dgrad(dz, fc1, lo1, dT1, ctx.sl1, ctx.training)
-        dh, _, _, _ = K.layer_norm_bwd(da, h2, ln_w, mean, rstd, dres=gh2)
-        return (dh.view(ctx.shp),) + (None,) * 12 + tuple(lg1) + tuple(lg2)
+        dh = _ln_bwd(ctx.hand_out, da, h2, ln_w, mean, rstd, gh2)
+        return (dh.view(ctx.shp),) + (None,) * 14 + tuple(lg1) + tuple(lg2)
 
 
-def mlp(h, ln, fc1, fc2, act, p, seed, seed_l1=0, seed_l2=0, training=True):
+def mlp(h, ln, fc1, fc2, act, p, seed, seed_l1=0, seed_l2=0, training=True, handoff=None):
+    """h + dropout(fc2(act(fc1(LN(h))))).  ``handoff``: this op's LN backward also runs the residual-dropout
+    backward of the linear_residual that produced h; the output carries a GradHandoff of its own for the
+    next block's ln_linear (attribute ``_mift_hand``)."""
     fast = _infer_ln_gemm(h, ln, fc1)
     if fast is not None and not training:  # decode: LN inside fc1's skinny GEMM, no pre-activation store
         h2, w1 = fast
@@ -501,8 +565,12 @@ def mlp(h, ln, fc1, fc2, act, p, seed, seed_l1=0, seed_l2=0, training=True):
         out = K.gemm(f, fc2.w_nk(), fc2.bias, T2, lo2.B32 if lo2 else None, residual=h2)
         return out.view(h.shape)
     l1, l2 = fc1.lora_params(), fc2.lora_params()
-    return MLP.apply(h, ln.weight, ln.bias, fc1, fc2, ln.eps, act, p, seed, seed_l1, seed_l2, training, len(l1),
-                     *l1, *l2)
+    hand_in = GradHandoff() if (training and l2 and torch.is_grad_enabled()) else None
+    out = MLP.apply(h, ln.weight, ln.bias, fc1, fc2, ln.eps, act, p, seed, seed_l1, seed_l2, training, len(l1),
+                    handoff, hand_in, *l1, *l2)
+    if hand_in is not None:
+        out._mift_hand = hand_in
+    return out
 
 
 # ---------------------------------------------------------------------------

@@ -139,6 +139,16 @@ def layer_norm_fwd_proj(x, w, b, eps, pw, rank, alpha=1.0, p=0.0, seed=0):
     return C().layer_norm_fwd_proj(x, w, b, float(eps), pw, int(rank), float(alpha), float(p), int(seed))
 
 
+def ln_bwd_mask_proj_ok(D):
+    return bool(C().ln_bwd_mask_proj_ok(int(D)))
+
+
+def ln_bwd_mask_proj(dy, x, w, mean, rstd, dres, p, seed, pw, rank, alpha=1.0):
+    """(dh, y, proj): dh = layer_norm_bwd(dy; x, w, mean, rstd) + dres, then mask_proj(dh, p, seed, pw, rank,
+    alpha) in the same row pass (csrc/kernels/rowproj.hip MODE 3)."""
+    return C().ln_bwd_mask_proj(dy, x, w, mean, rstd, dres, float(p), int(seed), pw, int(rank), float(alpha))
+
+
 def mask_proj(x, p, seed, pw, rank, alpha=1.0):
     """(y, proj[M,32]) = dropout(x) (x itself when p == 0), alpha·y·pwᵀ — dropout-bwd fused with dT."""
     return C().mask_proj(x, float(p), int(seed), pw, int(rank), float(alpha))
