@@ -223,7 +223,7 @@ def test_fused_backward_notifies_dp_reducer_per_layer(monkeypatch):
 def test_ln_backward_handoff_fires_and_matches_separate_passes(monkeypatch):
     """GradHandoff: at D = 768 every LN backward that feeds a LoRA linear's residual-dropout backward runs
     them as one pass (ln_bwd_mask_proj: the MLP's LN for attn.c_proj in every block, the next block's
-    ln_1 for mlp.c_proj), and the LoRA gradients match the separate LN-bwd + mask_proj passes."""
+    ln_1 — or the head's ln_f — for mlp.c_proj), and the LoRA gradients match the separate LN-bwd + mask_proj passes."""
     from mift.ops import kernels as K
     cfg = GPT2Config(vocab_size=1000, n_positions=128, n_embd=768, n_layer=3, n_head=12, n_inner=3072,
                      embd_pdrop=0.1, attn_pdrop=0.1, resid_pdrop=0.1)
@@ -247,9 +247,9 @@ def test_ln_backward_handoff_fires_and_matches_separate_passes(monkeypatch):
         return [p.grad.float().clone() for _, p in L.lora_parameters(m)]
 
     g1 = grads(True)
-    assert len(calls) == 2 * cfg.n_layer - 1, len(calls)
+    assert len(calls) == 2 * cfg.n_layer, len(calls)  # + the final LN's (fused LM head) for the last mlp
     g0 = grads(False)
-    assert len(calls) == 2 * cfg.n_layer - 1
+    assert len(calls) == 2 * cfg.n_layer
     for a, b in zip(g1, g0):
         rel = (a - b).norm() / (b.norm() + 1e-6)
         assert rel < 2e-2, rel

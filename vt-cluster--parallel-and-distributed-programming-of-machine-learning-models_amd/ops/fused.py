@@ -607,6 +607,7 @@ class LMHeadXent(torch.autograd.Function):
         if need_grad:
             ctx.save_for_backward(h2, mean, rstd, ln_w, E, stats, lse, lab)
         ctx.shp, ctx.w_nk, ctx.w_kn, ctx.V, ctx.shift, ctx.ign = shp, w_nk, w_kn, V, shift, ign
+        ctx.hand = getattr(h, "_mift_hand", None)  # the last block's mlp dropout-bwd rides on the final LN's
         ctx.gmul = _HEAD_GMUL[0]
         if ctx.gmul is not None:
             _HEAD_GMUL[1] = True
@@ -619,7 +620,7 @@ class LMHeadXent(torch.autograd.Function):
         g1 = g.reshape(1)
         da = K.lmhead_dgrad(E, w_kn, ctx.w_nk, lab, ctx.V, stats, lse, g1 if g1.dtype == torch.float32 else g1.float(),
                             ctx.shift, ctx.ign, ctx.gmul)
-        dh, _, _, _ = K.layer_norm_bwd(da, h2, ln_w, mean, rstd)
+        dh = _ln_bwd(ctx.hand, da, h2, ln_w, mean, rstd, None)
         return dh.view(ctx.shp), None, None, None, None, None, None, None, None, None, None
 
 
