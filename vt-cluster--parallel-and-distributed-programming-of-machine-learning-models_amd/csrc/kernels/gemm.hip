@@ -78,6 +78,13 @@ struct LmArgs {
   int nt;                 // MIFT_LM_NT (A/B): bit 0 = nontemporal E stores (fwd), bit 1 = nt E loads (dgrad)
   int shift;              // > 0: labels are the UNSHIFTED [B*S] ids, S = shift (see lm_label)
   int64_t ignore;         // >= 0: this id is no target (OPT ignores its pad id, a real vocabulary entry)
+  // dgrad in-launch reduction (fin != nullptr): the chunk blocks of a tile store their slabs write-through
+  // and the last to arrive (counter fin[tile]) applies lmhead_reduce_kernel's arithmetic to the tile
+  unsigned* fin;
+  const float* gmul;      // optional 1/tokens of a replayed step
+  const void* w;          // [V_pad, N] (rows = the one-hot part W[label])
+  int ldw;
+  void* dx;               // [M, N] output
 };
 
 // Target of row `row`: with shift = S the labels tensor holds the unshifted ids and row r's target
@@ -412,7 +419,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         const int r = i * 8 + srow;
         const int gr = min(r00 + r, rmax);
         const void* src = (const void*)(G + (size_t)gr * ld + (kb + t) * BK + (spc ^ (r & 7)) * 8);
-        if (EPI == 2 && o == 0 && (ep.lm.nt & 2))  // E is streamed once: keep W resident in L2
+        if ((EPI == 2 || EPI == 4) && o == 0 && (ep.lm.nt & 2))  // E is streamed once: keep W resident in L2
           __builtin_amdgcn_global_load_lds(src, (void*)(base + i * 1024), 16, 0, 2);
         else
           __builtin_amdgcn_global_load_lds(src, (void*)(base + i * 1024), 16, 0, 0);
@@ -864,7 +871,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       lm_fwd_epilogue();
     }
     return;
-  } else if constexpr (EPI == 2) {
+  } else if constexpr (EPI == 2 || EPI == 4) {  // 4: + the in-launch reduction (opt-in, MIFT_LM_FIN=1)
     // ---- LM-head dgrad on the phased 256x256 tile.  A = E [M, V_pad], B = Wᵀ [N, V_pad].
     // Each group of GK k-tiles is one forward column tile j whose E is relative to its own max
     // m_j.  Flash-style, acc is kept relative to a per-row reference ref: at every group start
@@ -918,6 +925,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       });
     }
     float* dst = lm.partial + (size_t)cidx * M * N;
+    constexpr bool fin = EPI == 4;  // a separate instantiation: the default kernel carries none of it
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = m0 + wm * WM + i * 16 + fr;
@@ -926,8 +934,48 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + wn * WN + j * 16 + fq * 4;
-        if (col < N) *reinterpret_cast<float4_*>(dst + (size_t)row * N + col) = acc[i][j] * fac;
+        if (col < N) {
+          if (fin)  // byte offset < 2^31 (host-checked)
+            mift_st16_sc1(lm.partial, (uint32_t)((((size_t)cidx * M + row) * N + col) * 4), acc[i][j] * fac);
+          else
+            *reinterpret_cast<float4_*>(dst + (size_t)row * N + col) = acc[i][j] * fac;
+        }
       }
+    }
+    if constexpr (!fin) return;
+    __shared__ int lm_last;
+    if (!mift_group_arrival(lm.fin + tl, (unsigned)S, &lm_last)) return;
+    // the tile's last chunk block: slabs summed in chunk order, one-hot part, upstream gradient — the
+    // arithmetic of lmhead_reduce_kernel (bit-identical), without its launch and its cold re-read
+    const float gsc = lm.gmul ? lm.gscale[0] * lm.gmul[0] : lm.gscale[0];
+    const T* wl = reinterpret_cast<const T*>(lm.w);
+    T* dxo = reinterpret_cast<T*>(lm.dx);
+    constexpr int CPT = BN / 8;
+    for (int v = tid; v < BM * CPT; v += NT) {
+      const int row = m0 + v / CPT, c8 = n0 + (v % CPT) * 8;
+      if (row >= M || c8 >= N) continue;
+      float a8[8];
+      {
+        const float4* p = reinterpret_cast<const float4*>(lm.partial + (size_t)row * N + c8);
+        const float4 a = p[0], b = p[1];
+        a8[0] = a.x; a8[1] = a.y; a8[2] = a.z; a8[3] = a.w; a8[4] = b.x; a8[5] = b.y; a8[6] = b.z; a8[7] = b.w;
+      }
+      for (int q = 1; q < S; ++q) {
+        const float4* p = reinterpret_cast<const float4*>(lm.partial + ((size_t)q * M + row) * N + c8);
+        const float4 a = p[0], b = p[1];
+        a8[0] += a.x; a8[1] += a.y; a8[2] += a.z; a8[3] += a.w; a8[4] += b.x; a8[5] += b.y; a8[6] += b.z; a8[7] += b.w;
+      }
+      const int64_t lab = lm_label(lm.labels, row, lm.shift, lm.ignore);
+      if (lab >= 0 && lab < lm.V) {
+        float wv[8];
+        load8<T>(wl + (size_t)lab * lm.ldw + c8, wv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a8[e] = gsc * (a8[e] - wv[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a8[e] = 0.f;
+      }
+      store8<T>(dxo + (size_t)row * N + c8, a8);
     }
     return;
   } else if constexpr (!SKM) {
@@ -1712,6 +1760,15 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   return {E, stats, lse, loss, zlab};
 }
 
+// per-tile arrival counters of the LM-head dgrad's in-launch reduction (zeroed once, re-armed by each
+// tile's last chunk block; first allocated by an eager call, outside any capture)
+unsigned* lm_fin_flags(int n) {
+  static at::Tensor flags;
+  if (!flags.defined() || flags.numel() < n)
+    flags = at::zeros({std::max<int64_t>(n, 1 << 12)}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA));
+  return reinterpret_cast<unsigned*>(flags.data_ptr<int>());
+}
+
 template <typename T>
 at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
                              int V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale, int shift,
@@ -1744,16 +1801,33 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   ep.lm.ignore = ignore;
   if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   SkArgs sk{};
-  auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
+  auto kern2 = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
+  auto kern4 = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 4>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)kern2, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)kern4, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr = true;
   }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-  hipLaunchKernelGGL(kern, dim3(tiles * S), dim3(512), SMEM, st, (const T*)E.data_ptr(), (const T*)wt.data_ptr(),
-                     (T*)nullptr, nullptr, nullptr, M, N, K, (int)E.stride(0), (int)wt.stride(0), N, ep, sk);
   auto out = at::empty({M, N}, E.options());
+  // in-launch reduction by each tile's last chunk block: opt-in (MIFT_LM_FIN=1), bit-identical but
+  // slower — distilgpt2 head 1.42 -> 1.59 ms, step +0.17 ms: the 201 MB of write-through slab stores and
+  // the finishers' serial tail cost more than the 37 us launch they replace
+  // (profiles/r4/lmhead_in_launch_reduction_rejected.txt)
+  const char* fe = getenv("MIFT_LM_FIN");
+  const bool fin = fe && atoi(fe) == 1 && (size_t)S * M * N * 4 < (1ull << 31);
+  if (fin) {
+    ep.lm.fin = lm_fin_flags(tiles);
+    ep.lm.gmul = gmul ? gmul->data_ptr<float>() : nullptr;
+    ep.lm.w = w.data_ptr();
+    ep.lm.ldw = (int)w.stride(0);
+    ep.lm.dx = out.data_ptr();
+  }
+  hipLaunchKernelGGL(fin ? kern4 : kern2, dim3(tiles * S), dim3(512), SMEM, st, (const T*)E.data_ptr(),
+                     (const T*)wt.data_ptr(), (T*)nullptr, nullptr, nullptr, M, N, K, (int)E.stride(0),
+                     (int)wt.stride(0), N, ep, sk);
+  if (fin) return out;
   const size_t chunks = (size_t)M * (N / 8);
   hipLaunchKernelGGL(lmhead_reduce_kernel<T>, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st,
                      partial.data_ptr<float>(), S, M, N, (const T*)w.data_ptr(), (int)w.stride(0),
