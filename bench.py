@@ -83,7 +83,8 @@ def parse_args(argv=None):
     ap.add_argument("--epoch_lines", type=int, default=None,
                     help="after the timed steps, run one full epoch over this many medium_openwebtext-shaped "
                          "lines (README.md:66: ~20k) sharded over the DP ranks and report its wall clock "
-                         "(the reference's [Training] sec metric); default 20000 for GPT-2, 0 (skip) for OPT")
+                         "(the reference's [Training] sec metric, P1 and P2 alike: P2/summarize_opt_times.py:39-51); "
+                         "default 20000, 0 skips it")
     a = ap.parse_args(argv)
     c = dict(CONFIGS[a.config])
     if a.model and a.model != c["model"]:  # a model override keeps that family's reference precision
@@ -97,7 +98,7 @@ def parse_args(argv=None):
     a.steps = a.steps if a.steps is not None else c.get("steps", 50)
     a.warmup = a.warmup if a.warmup is not None else c.get("warmup", 10)
     if a.epoch_lines is None:
-        a.epoch_lines = c.get("epoch_lines", 0 if "opt" in a.model.lower() else 20000)
+        a.epoch_lines = c.get("epoch_lines", 20000)
     if a.micro_batch == "0" and a.pp > 1:
         a.micro_batch = "auto"
     if a.virtual is None:

@@ -179,3 +179,68 @@ def test_partition_rules():
     b = partition_layers(32, 4, "balanced", head_layers=1.6)
     assert sum(b) == 32 and b[-1] < 8 and max(b[:-1]) <= 9
     assert sum(partition_layers(32, 8, "balanced", head_layers=1.6)) == 32
+
+
+def test_interleaved_blocking_p2p_mode(single_drop):
+    """MIFT_PP_P2P=blocking with the interleaved schedule: receives posted just in time (no one-op
+    prefetch — under blocking receives that prefetch deadlocks at S = 2, V = 2, M = 2)."""
+    r = harness.run(_worker, 2, pp=2, dropout=0.1, virtual=2, p2p="blocking")
+    _close_runs(r[0], single_drop)
+    # M = 2 micro-batches per step: the case the prefetch deadlocked; same result as the default layout
+    a = harness.run(_worker, 2, pp=2, dropout=0.1, virtual=2, p2p="blocking", accum=2, mb=4)
+    b = harness.run(_worker, 2, pp=2, dropout=0.1, virtual=2, accum=2, mb=4)
+    _close_runs(a[0], b[0])
+
+
+def test_chunk_slot_counts_cover_in_flight_micro_batches():
+    """Interleaved stage graphs: slot i % K_c of chunk c is free again (its backward queued) before
+    micro-batch i + K_c's receive is posted, for both receive policies."""
+    from mift.parallel.pipeline import chunk_slot_counts, schedule_interleaved
+    for S, V, M in [(2, 2, 2), (2, 2, 4), (4, 2, 8), (4, 4, 24), (8, 2, 16), (3, 3, 6)]:
+        for pre in (True, False):
+            for s in range(S):
+                K = chunk_slot_counts(S, s, M, V, prefetch=pre)
+                ops = schedule_interleaved(S, s, M, V)
+                owner = [dict() for _ in range(V)]
+                for j, (op, c, i) in enumerate(ops):
+                    for jj in ((j, j + 1) if pre else (j,)):
+                        if jj < len(ops) and ops[jj][0] == "F":
+                            cc, ii = ops[jj][1], ops[jj][2]
+                            k = ii % K[cc]
+                            assert owner[cc].get(k, ii) == ii, (S, V, M, s, cc, ii)
+                            owner[cc][k] = ii
+                    if op == "B":
+                        assert owner[c].pop(i % K[c]) == i
+                assert all(k <= M for k in K)
+
+
+def test_partition_balanced_by_rank():
+    """Rank-balanced split for the interleaved pipeline (ranks=): every chunk keeps >= 1 layer, the
+    layers sum up, and the last rank (which carries the head) holds fewer layers than the others."""
+    for L_, S, V, head in [(32, 4, 4, 1.6), (32, 4, 2, 1.6), (32, 8, 2, 1.2), (24, 4, 2, 3.0), (8, 2, 2, 0.4)]:
+        split = partition_layers(L_, S * V, "balanced", head_layers=head, ranks=S)
+        assert sum(split) == L_ and min(split) >= 1 and len(split) == S * V, split
+        per_rank = [sum(split[c * S + r] for c in range(V)) for r in range(S)]
+        if int(head + 0.5) >= 1:
+            assert per_rank[-1] < max(per_rank[:-1]), (split, per_rank)
+        assert max(per_rank) - min(per_rank[:-1]) <= 1, (split, per_rank)
+
+
+def _groups_worker(rank, world, mode, virtual=1):
+    import os
+    os.environ["MIFT_PP_P2P"] = mode
+    from mift.parallel import dist as D
+    ctx = D.init(pp=world, verbose=False, sanity=False, virtual=virtual)
+    out = {"n": ctx.n_groups, "shared": ctx.pp_fwd_group is not None, "link": ctx.link_f != [None, None]}
+    D.destroy()
+    return out
+
+
+@pytest.mark.parametrize("mode,virtual,n", [("link", 1, 1 + 2 * 3), ("blocking", 1, 1 + 2 * 3), ("shared", 1, 3),
+                                            ("link", 2, 1 + 2 * 3 + 2)])
+def test_grid_creates_only_the_selected_p2p_groups(mode, virtual, n):
+    """4 pipeline ranks: the pipe group, then per-link pairs (link / blocking) OR the two replica-wide
+    communicators (shared), plus the wrap-around pair when interleaved — never both layouts."""
+    r = harness.run(_groups_worker, 4, mode=mode, virtual=virtual)
+    assert r[0]["n"] == n, r
+    assert r[0]["shared"] == (mode == "shared") and r[0]["link"] == (mode != "shared")

@@ -79,10 +79,21 @@ def test_pipeline_graphs_match_eager_and_single(single, pp):
 
 def test_interleaved_pipeline_on_gpu(single):
     """Interleaved 1F1B on the fused GPU kernels: 2 ranks x 2 model chunks (4 virtual stages of one
-    layer each; chunk 0's activations return from rank 1 to rank 0 over the wrap-around link),
-    eager, == the single-process run."""
+    layer each; chunk 0's activations return from rank 1 to rank 0 over the wrap-around link), eager
+    == the single-process run, and the per-(chunk, slot) stage graphs (steps 2-3 replay) == eager."""
     r = harness.run(_worker, 2, env=GPU_ENV, timeout=240, pp=2, virtual=2)
     _close(r[0], single, 2e-3)
+    g = harness.run(_worker, 2, env=GPU_ENV, timeout=240, pp=2, virtual=2, graph=True)
+    for k in range(2):
+        assert g[k]["stats"]["replays"] > 0 and r[k]["stats"]["replays"] == 0, (g[k]["stats"], r[k]["stats"])
+    _close(g[0], r[0], 1e-3)
+
+
+def test_interleaved_graphs_blocking_p2p(single):
+    """The interleaved graphs with MIFT_PP_P2P=blocking (just-in-time receives) == single."""
+    g = harness.run(_worker, 2, env=GPU_ENV, timeout=240, pp=2, virtual=2, graph=True, p2p="blocking")
+    assert g[0]["stats"]["replays"] > 0
+    _close(g[0], single, 2e-3)
 
 
 @pytest.mark.parametrize("p2p", ["shared", "blocking"])

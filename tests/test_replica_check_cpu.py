@@ -44,3 +44,40 @@ def test_ulp_drift_is_tolerated_and_resynced():
 def test_real_divergence_raises_with_tolerance(delta):
     r = harness.run(_w, 2, timeout=120, delta=delta, rtol=1e-5)
     assert all(x["err"] and "spread" in x["err"] for x in r)
+
+
+def _w_slices(rank, world):
+    from mift.parallel import dist as D
+    from mift.parallel.ddp import verify_replicas
+    D.init(verbose=False, sanity=False)
+    big = torch.linspace(-1.0, 1.0, 1000)
+    small = torch.full((100,), 1e-6)          # e.g. LoRA B early in training
+    t = torch.cat([big, small])
+    m = torch.zeros(1100)
+    if rank == 1:
+        t[1050] += 1e-6    # 100 % of the small slice's scale, 1e-6 of the arena's
+        m[5] = 1.0
+    out = {}
+    for name, sl in [("whole", None), ("sliced", [[(0, 1000), (1000, 100)]])]:
+        try:
+            verify_replicas([t.clone()], rtol=1e-5, resync=False, slices=sl)
+            out[name] = None
+        except RuntimeError as e:
+            out[name] = str(e)
+    t2 = torch.linspace(-1.0, 1.0, 1000)
+    if rank == 1:
+        t2[3] += 1e-7
+    verify_replicas([t2], rtol=1e-5, resync=True, companions=[[m]])
+    out["m_synced"] = float(m[5])
+    D.destroy()
+    return out
+
+
+def test_spread_is_judged_per_parameter_slice():
+    """A real divergence inside a small-magnitude slice passes the arena-wide scale but not the per-slice
+    one; a resync also re-broadcasts the companion optimizer state."""
+    r = harness.run(_w_slices, 2, timeout=120)
+    for x in r:
+        assert x["whole"] is None
+        assert x["sliced"] and "slice [1000, 1100)" in x["sliced"]
+        assert x["m_synced"] == 0.0

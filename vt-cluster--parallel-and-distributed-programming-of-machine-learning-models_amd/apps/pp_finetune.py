@@ -57,14 +57,18 @@ def build_argparser():
     ap.add_argument("--ds_cfg", default="deepspeed_pp_zero1_cpu.json")
     # mift extensions
     ap.add_argument("--pp", type=int, default=None, help="pipeline stages (default $PIPELINE_PARALLEL_SIZE or world)")
-    ap.add_argument("--virtual_stages", type=int, default=None,
-                    help="interleaved 1F1B: model chunks per pipeline rank (default $PIPELINE_VIRTUAL_STAGES or 1)")
+    ap.add_argument("--virtual_stages", default=None,
+                    help="interleaved 1F1B: model chunks per pipeline rank, or 'auto' (chosen with the micro-batch "
+                         "by the planner); default $PIPELINE_VIRTUAL_STAGES, mift.virtual_stages, else 'auto' when "
+                         "the micro-batch is planned and 1 otherwise")
     ap.add_argument("--partition", choices=["uniform", "balanced"], default=None,
                     help="layer split (default: mift.pp_partition / pipeline.partition_method, else balanced)")
     ap.add_argument("--precision", choices=["fp16", "bf16", "fp32"], default=None)
-    ap.add_argument("--micro_batch", type=int, default=0,
+    ap.add_argument("--micro_batch", default=None,
                     help="GPU micro-batch: regroups batch*accum sequences per step into micro-batches of this "
-                         "size (same token-normalised update, fewer pipeline bubbles); 0 = keep --batch")
+                         "size (same token-normalised update, fewer pipeline bubbles); 'auto' = the planner "
+                         "(mift.parallel.plan, measured dp1 cost curve + HBM bound; the default on GPU with "
+                         ">1 stage, or mift.micro_batch); 0 = keep the DeepSpeed / --batch micro-batch")
     ap.add_argument("--zero", type=int, default=None, help="ZeRO stage override (0/1)")
     ap.add_argument("--synthetic", type=int, default=-1, help="N synthetic lines (-1: only if data file missing)")
     ap.add_argument("--base_weights", default=None)
@@ -92,23 +96,66 @@ def read_ds_config(path):
     return MiftConfig.from_json(path)
 
 
+def _will_use_gpu():
+    if os.environ.get("MIFT_DEVICE", "") == "cpu":
+        return False
+    return torch.cuda.device_count() > 0  # counting devices does not initialise HIP
+
+
+def plan_micro_batch(args, ds, stages, world, gpu):
+    """Resolve (GPU micro-batch, virtual stages, plan) before the process grid is built (interleaving
+    needs the wrap-around links).  The reference CLI (``--batch 1 --accum 96``) on a GPU pipeline runs
+    the planner's micro-batch: micro-batch 1 leaves MI355X's matrix cores idle (OPT-2.7B 25.5 ms per
+    sequence at mb 1 vs 6.8 at mb 12, parallel/plan.py MEASURED) — the token-normalised update is the
+    same for any regrouping of the batch*accum sequences of a step."""
+    mbsel = args.micro_batch if args.micro_batch is not None else ds.micro_batch
+    if mbsel in (0, "0", None) and args.micro_batch is None and gpu and stages > 1:
+        mbsel = "auto"
+    mbsel = "auto" if str(mbsel).lower() == "auto" else int(mbsel or 0)
+    vsel = args.virtual_stages or os.environ.get("PIPELINE_VIRTUAL_STAGES") or ds.virtual_stages
+    if vsel is None:
+        vsel = "auto" if mbsel == "auto" else 1
+    vsel = "auto" if str(vsel).lower() == "auto" else int(vsel)
+    base_mb = ds.micro_batch_size or args.batch
+    per_step = base_mb * args.accum          # sequences per optimizer step per DP replica
+    plan = None
+    if stages > 1 and (mbsel == "auto" or vsel == "auto"):
+        from ..models.opt import OPTConfig
+        from ..parallel.plan import choose_micro_batch
+        cfg = OPTConfig.preset(args.model_name)
+        plan = choose_micro_batch(cfg, args.seq_len, per_step, stages, dtype_bytes=2, name=args.model_name,
+                                  candidates=None if mbsel == "auto" else [mbsel or base_mb],
+                                  virtual=vsel)
+        mbsel, vsel = plan["micro_batch"], plan["virtual"]
+    elif mbsel == "auto":
+        mbsel = 0
+    if vsel == "auto":
+        vsel = 1
+    return (mbsel or 0), int(vsel), plan
+
+
 def main(argv=None):
     args, _unknown = build_argparser().parse_known_args(argv)
     world_env = int(os.environ.get("WORLD_SIZE", os.environ.get("SLURM_NTASKS", "1")))
     stages = args.pp or int(os.environ.get("PIPELINE_PARALLEL_SIZE", str(world_env)))
     assert 1 <= stages <= 32, "PIPELINE_PARALLEL_SIZE must be in [1,32]"
-    ctx = D.init(pp=stages, virtual=args.virtual_stages)
+    ds = read_ds_config(args.ds_cfg)
+    gmb, virtual, plan = plan_micro_batch(args, ds, stages, world_env, _will_use_gpu())
+    ctx = D.init(pp=stages, virtual=virtual)
     rank = ctx.rank
 
     def log(msg):
         print(f"[R{rank}] {msg}", flush=True)
 
     gpu = ctx.device.type == "cuda"
-    ds = read_ds_config(args.ds_cfg)
     ds.apply_env()
     if rank == 0:
         for line in ds.report():
             print(line, flush=True)
+        if plan is not None:
+            print(f"[R0] micro-batch plan: mb={plan['micro_batch']} virtual={plan['virtual']} "
+                  f"predicted step {plan['step_ms']} ms, per-GPU efficiency vs dp1 {plan['efficiency_vs_dp1']}, "
+                  f"activations {plan['act_gib']} GiB", flush=True)
     precision = args.precision or ("fp32" if not gpu else ("bf16" if ds.bf16 else "fp16"))
     if not gpu:
         precision = "fp32"
@@ -167,7 +214,6 @@ def main(argv=None):
     t0 = time.perf_counter()
     mb = ds.micro_batch_size or args.batch
     per_step = mb * args.accum
-    gmb = args.micro_batch or ds.micro_batch
     if gmb and per_step % gmb == 0:
         mb = gmb
     accum = per_step // mb
@@ -212,7 +258,8 @@ def main(argv=None):
         if tok is not None:
             tok.save_pretrained(out)
         with open(os.path.join(out, "meta.json"), "w") as f:
-            json.dump({"split": split, "stages": ctx.pp, "virtual_stages": ctx.pp_virtual}, f, indent=2)
+            json.dump({"split": split, "stages": ctx.pp, "virtual_stages": ctx.pp_virtual, "micro_batch": mb,
+                       "micro_batches_per_step": accum, "micro_batch_plan": plan}, f, indent=2)
         log(f"Saved adapters+tokenizer to {out}")
     logs.log("Model save", time.perf_counter() - t0, echo=False)
     tokens = trainer.global_step * per_step * args.seq_len * ctx.dp
@@ -221,7 +268,7 @@ def main(argv=None):
               f"steps={trainer.global_step}", flush=True)
     D.destroy()
     return {"train_seconds": train_secs, "steps": trainer.global_step, "save_dir": out, "split": split,
-            "history": trainer.history}
+            "history": trainer.history, "micro_batch": mb, "virtual_stages": ctx.pp_virtual, "plan": plan}
 
 
 if __name__ == "__main__":

@@ -128,6 +128,7 @@ def main(argv=None):
     ap.add_argument("--weights", default=None, help="local HF checkpoint dir of the generator")
     ap.add_argument("--tokenizer", default=None, help="local HF T5 tokenizer dir")
     ap.add_argument("--fallback_retriever", action="store_true")
+    ap.add_argument("--show_passages", action="store_true", help="also print the retrieved passages (score, text)")
     args, _ = ap.parse_known_args(argv)
     from ..data.agnews import load_split
     n = min(args.subset, 2000) if args.dry_run else args.subset
@@ -163,6 +164,9 @@ def main(argv=None):
             for q in shard[i:i + args.batch]:
                 a, hits = answer(q)
                 print(f"\nQ: {q}\nA: {a}", flush=True)
+                if args.show_passages:
+                    for i, sc in hits:
+                        print(f"   [{sc:.3f}] {corpus[i][:110]}", flush=True)
                 results.append((q, a, hits))
         return results
     print("Nothing to do: provide --query '...' or --queries_file <path>.")

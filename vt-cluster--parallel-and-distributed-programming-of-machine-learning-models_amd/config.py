@@ -17,7 +17,9 @@ Reference: P2 loads a DeepSpeed JSON (``--ds_cfg``,
 * ``mift`` section (MI355X-specific, defaults sized for one process per GPU over xGMI):
   ``kernels`` (HIP kernels on/off), ``graph`` (hipGraph replay: auto/on/off), ``lmhead``
   (fused | blas), ``bucket_mb`` (DP all-reduce bucket), ``pp_partition`` (uniform | balanced),
-  ``pp_schedule`` (1f1b), ``micro_batch`` (GPU micro-batch regrouping), ``side_stream``
+  ``pp_schedule`` (1f1b), ``micro_batch`` (GPU micro-batch regrouping: an int, or "auto" = the
+  pipeline planner ``mift.parallel.plan.choose_micro_batch``), ``virtual_stages`` (interleaved 1F1B
+  chunks per pipeline rank: an int, or "auto" = chosen with the micro-batch), ``side_stream``
   (LoRA weight grads on a second stream), ``comm_timeout_s`` (collective watchdog),
   ``consistency_every`` (replica checksum period), ``max_inflight_steps`` (host run-ahead bound);
 * anything else is an error unless ``mift.strict`` is false (then a warning).
@@ -48,7 +50,8 @@ _NO_EFFECT = {
     "steps_per_print": "logging_steps / --log_every control logging",
     "wall_clock_breakdown": "phase timers are always on (timing_rank*.log)",
 }
-_MIFT_KEYS = {"kernels", "graph", "lmhead", "bucket_mb", "pp_partition", "pp_schedule", "micro_batch", "side_stream",
+_MIFT_KEYS = {"kernels", "graph", "lmhead", "bucket_mb", "pp_partition", "pp_schedule", "micro_batch", "virtual_stages",
+              "side_stream",
               "comm_timeout_s", "consistency_every", "max_inflight_steps", "strict"}
 
 
@@ -76,7 +79,8 @@ class MiftConfig:
     bucket_mb: float = 25.0
     pp_partition: str = "balanced"
     pp_schedule: str = "1f1b"
-    micro_batch: int = 0
+    micro_batch: object = 0          # int, or "auto" (planner); 0 = the DeepSpeed micro-batch as is
+    virtual_stages: object = None    # int, or "auto"; None = the app's default
     side_stream: Optional[bool] = None
     comm_timeout_s: Optional[int] = None
     consistency_every: int = 0
@@ -139,7 +143,10 @@ class MiftConfig:
         c.bucket_mb = float(m.get("bucket_mb", 25.0))
         c.pp_partition = str(m.get("pp_partition", c.pp_partition))
         c.pp_schedule = str(m.get("pp_schedule", "1f1b"))
-        c.micro_batch = int(m.get("micro_batch", 0))
+        mb = m.get("micro_batch", 0)
+        c.micro_batch = "auto" if str(mb).lower() == "auto" else int(mb)
+        vs = m.get("virtual_stages")
+        c.virtual_stages = None if vs is None else ("auto" if str(vs).lower() == "auto" else int(vs))
         c.side_stream = m.get("side_stream")
         c.comm_timeout_s = m.get("comm_timeout_s")
         c.consistency_every = int(m.get("consistency_every", 0))

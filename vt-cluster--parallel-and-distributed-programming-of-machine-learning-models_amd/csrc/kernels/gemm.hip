@@ -1054,6 +1054,260 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   }  // SKM
 }
 
+// ---- persistent fused LM-head forward (EPI 1's arithmetic; default, MIFT_LM_PERSIST=0: the one-tile kernel) ----
+// The distilgpt2 head is 6,304 tiles of 256x256 at K = 768: 12 k-tiles of main loop per tile, after which
+// the one-tile kernel runs its epilogue (row maxima, exp, E store) and its block exits; the next block's
+// prologue then refills the ring from nothing.  Here one 512-thread block per CU
+// walks the tiles xb, xb + G, ... (G = grid, xb = XCD-remapped block id: the 32 blocks sharing an XCD
+// take 32 consecutive tile slots, as the one-tile launch placed them) as ONE continuous k-tile stream:
+// the phased 4-phase schedule of mainloop8 issues k-tile g+1's A halves and g+2's B halves whatever tile
+// they belong to, so when a tile's last k-tile retires, the next tile's first k-tile is already in LDS
+// and its second in flight while the epilogue runs.  The epilogue keeps E out of LDS (the ring is busy
+// with the next tile): each lane packs its 4-column fragments to 16 bits and one v_permlane16_swap per
+// dword pairs lanes l / l^16 so every lane holds 8 consecutive columns -> one 16-B store per lane and
+// row-fragment pair (16 rows x 64 contiguous bytes per instruction, whole 128-B lines per wave).  Only
+// the cross-wave row maxima / sums and the row targets go through a 9 KiB LDS side area behind the
+// ring; its barriers are raw s_barriers (a __syncthreads would drain the in-flight LDS-DMA and E stores).
+template <typename T>
+__global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                                  T* __restrict__ E, int M, int N, int K, int lda,
+                                                                  int ldb, int lde, LmArgs lm, int ntiles, int group_m) {
+  constexpr int BM = 256, BN = 256, NWN = 4, NW = 8, WM = 128, WN = 64, TM = 8, TN = 4;
+  constexpr int A_BYTES = BM * ROWB, STAGE_BYTES = (BM + BN) * ROWB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* redm = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);  // [NW][WM] wave row maxima
+  float* reds = redm + NW * WM;                                     // [NW][WM] wave row sums
+  int* labs = reinterpret_cast<int*>(reds + NW * WM);               // [BM] row targets
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / NWN, wn = wave % NWN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int srow = lane >> 3, spc = lane & 7;
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
+  const int nk = K / BK;  // >= 2 (host-checked)
+  const int G = gridDim.x;
+  int xb;
+  {
+    const int q = G / 8, r = G % 8, xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
+    xb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int ntl = (ntiles - xb + G - 1) / G;  // G <= ntiles: every block owns >= 1 tile
+  const int total = ntl * nk;
+  auto coords = [&](int j, int& m0, int& n0) {
+    int tm, tn;
+    raster(j * G + xb, ntm, ntn, group_m, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  auto stage_half = [&](int buf, int m0, int n0, int kt, int o, int h) {
+    char* base = smem + buf * STAGE_BYTES + o * A_BYTES;
+    const T* Gp = o ? B : A;
+    const int ld = o ? ldb : lda;
+    const int rmax = (o ? N : M) - 1;
+    const int r00 = o ? n0 : m0;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int i = 16 * h + wave + 8 * ii;
+      const int r = i * 8 + srow;
+      const int gr = min(r00 + r, rmax);
+      __builtin_amdgcn_global_load_lds((const void*)(Gp + (size_t)gr * ld + kt * BK + (spc ^ (r & 7)) * 8),
+                                       (void*)(base + i * 1024), 16, 0, 0);
+    }
+  };
+  float4_ acc[TM][TN];
+  frag_t<T> af[4][2], bq[4][2];
+  auto rd = [&](const char* p) { return *reinterpret_cast<const frag_t<T>*>(p); };
+  auto cluster = [&](int qi, int qj) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qi * 4 + i][qj * 2 + j] = mfma16<T>(bq[qj * 2 + j][kk], af[i][kk], acc[qi * 4 + i][qj * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto raw_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  constexpr float L2E = 1.4426950408889634f;
+  auto pack2 = [](float a, float b) {
+    T ta = (T)a, tb = (T)b;
+    unsigned short ua, ub;
+    __builtin_memcpy(&ua, &ta, 2);
+    __builtin_memcpy(&ub, &tb, 2);
+    return (unsigned)ua | ((unsigned)ub << 16);
+  };
+  // tile (m0, n0) epilogue from acc: E = exp(z - m_row,tile) 16-bit, (m, s) stats, the label's fp32 logit
+  auto epilogue = [&](int m0, int n0, auto fullc) {
+    constexpr bool FULL = decltype(fullc)::value;
+    const int V = lm.V;
+    if (tid < BM) {
+      const int64_t l = lm_label(lm.labels, min(m0 + tid, M - 1), lm.shift, lm.ignore);
+      labs[tid] = (l >= 0 && l < V) ? (int)l : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 16 + fq * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = (FULL || col + e < V) ? fmaxf(m, acc[i][j][e]) : m;
+      }
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      if (fq == 0) redm[wave * WM + i * 16 + fr] = m;
+    }
+    raw_barrier();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < NWN; ++w) m = fmaxf(m, redm[(wm * NWN + w) * WM + i * 16 + fr]);
+      if (m == -INFINITY) m = 0.f;
+      const int lrow = wm * WM + i * 16 + fr;
+      const int row = m0 + lrow;
+      const int lab = labs[lrow];
+      const float mb = m * L2E;
+      float s = 0.f, zl = 0.f;
+      bool hit = false;
+      unsigned pk[TN][2];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 16 + fq * 4;
+        float ev[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ev[e] = (FULL || col + e < V) ? __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][e], L2E, -mb)) : 0.f;
+          s += ev[e];
+        }
+        const int d = lab - col;
+        const float4_ a4 = acc[i][j];
+        const float v = d == 0 ? a4[0] : d == 1 ? a4[1] : d == 2 ? a4[2] : a4[3];
+        const bool h = d >= 0 && d < 4;
+        zl = h ? v : zl;
+        hit = hit || h;
+        pk[j][0] = pack2(ev[0], ev[1]);
+        pk[j][1] = pack2(ev[2], ev[3]);
+      }
+      if (hit && row < M) lm.zlab[row] = zl;
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (fq == 0) reds[wave * WM + i * 16 + fr] = s;
+      // lanes l (row quarter fq even) and l ^ 16 trade fragments: fq even ends with columns
+      // 32p + 8(fq>>1) .. +7, fq odd with 32p + 16 + 8(fq>>1) .. +7 of the wave's 64
+#pragma unroll
+      for (int p = 0; p < TN / 2; ++p) {
+        const auto r0 = __builtin_amdgcn_permlane16_swap(pk[2 * p][0], pk[2 * p + 1][0], false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(pk[2 * p][1], pk[2 * p + 1][1], false, false);
+        const int c0 = n0 + wn * WN + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8;
+        if (!(lm.dbg & 1) && row < M && (FULL || c0 < N)) {
+          const v4u32 val = {(unsigned)r0[0], (unsigned)r1[0], (unsigned)r0[1], (unsigned)r1[1]};
+          *reinterpret_cast<v4u32*>(E + (size_t)row * lde + c0) = val;
+        }
+      }
+    }
+    raw_barrier();
+    if (tid < BM) {  // one thread per block row: the NWN waves' partials of the row
+      const int wr = tid / WM, rr = tid % WM;
+      float m = -INFINITY, s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWN; ++w) {
+        m = fmaxf(m, redm[(wr * NWN + w) * WM + rr]);
+        s += reds[(wr * NWN + w) * WM + rr];
+      }
+      if (m == -INFINITY) m = 0.f;
+      if (m0 + tid < M) lm.stats[(size_t)(m0 + tid) * lm.ntn + n0 / BN] = make_float2(m, s);
+    }
+  };
+
+  int m0, n0, nm0 = 0, nn0 = 0;
+  coords(0, m0, n0);
+  if (ntl > 1) coords(1, nm0, nn0);
+  stage_half(0, m0, n0, 0, 0, 0);
+  stage_half(0, m0, n0, 0, 0, 1);
+  stage_half(0, m0, n0, 0, 1, 0);
+  stage_half(0, m0, n0, 0, 1, 1);
+  if (total > 1) {
+    stage_half(1, m0, n0, 1, 1, 0);
+    stage_half(1, m0, n0, 1, 1, 1);
+    wait_vmcnt<4>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier (mainloop8)
+  asm volatile("" ::: "memory");
+  const int arow = wm * WM + fr, brow = wn * WN + fr;
+  const int sw0 = (fq ^ (fr & 7)) << 4, sw1 = ((4 + fq) ^ (fr & 7)) << 4;
+  for (int j = 0; j < ntl; ++j) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < TN; ++q) acc[i][q] = float4_{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const int g = j * nk + kt;
+      const char* As = smem + (g & 1) * STAGE_BYTES;
+      const char* Bs = As + A_BYTES;
+      // k-tiles g+1 / g+2: this tile's or (wrapping past its last k-tile) the next tile's
+      const bool w1 = kt + 1 >= nk, w2 = kt + 2 >= nk;
+      const int k1 = w1 ? kt + 1 - nk : kt + 1, k2 = w2 ? kt + 2 - nk : kt + 2;
+      const int m1 = w1 ? nm0 : m0, n1 = w1 ? nn0 : n0, m2 = w2 ? nm0 : m0, n2 = w2 ? nn0 : n0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i][0] = rd(As + (arow + i * 16) * ROWB + sw0);
+        af[i][1] = rd(As + (arow + i * 16) * ROWB + sw1);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        bq[q][0] = rd(Bs + (brow + q * 16) * ROWB + sw0);
+        bq[q][1] = rd(Bs + (brow + q * 16) * ROWB + sw1);
+      }
+      if (g + 1 < total) stage_half((g + 1) & 1, m1, n1, k1, 0, 0);
+      cluster(0, 0);
+#pragma unroll
+      for (int q = 2; q < 4; ++q) {
+        bq[q][0] = rd(Bs + (brow + q * 16) * ROWB + sw0);
+        bq[q][1] = rd(Bs + (brow + q * 16) * ROWB + sw1);
+      }
+      if (g + 1 < total) stage_half((g + 1) & 1, m1, n1, k1, 0, 1);
+      cluster(0, 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i][0] = rd(As + (arow + (i + 4) * 16) * ROWB + sw0);
+        af[i][1] = rd(As + (arow + (i + 4) * 16) * ROWB + sw1);
+      }
+      cluster(1, 1);
+      if (g + 2 < total) {
+        stage_half(g & 1, m2, n2, k2, 1, 0);
+        stage_half(g & 1, m2, n2, k2, 1, 1);
+        wait_vmcnt<4>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      cluster(1, 0);
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();  // re-align the wave rows for the epilogue's barriers
+    asm volatile("" ::: "memory");
+    if (n0 + BN <= lm.V && !(lm.dbg & 4)) epilogue(m0, n0, std::true_type{});  // block-uniform
+    else epilogue(m0, n0, std::false_type{});
+    if (wm == 1 && j + 1 < ntl) __builtin_amdgcn_s_barrier();  // re-stagger for the next tile
+    asm volatile("" ::: "memory");
+    m0 = nm0;
+    n0 = nn0;
+    if (j + 2 < ntl) coords(j + 2, nm0, nn0);
+  }
+}
+
 int num_cus() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -1729,16 +1983,29 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   // staging ring (128 KiB) reused for the E tile + the two row-partial arrays
   constexpr int SMEM = std::max(2 * (BM + BN) * ROWB, BM * CTile<BN>::CLD * 2 + 2 * 8 * (BM / 2) * 4 + BM * 4);
   static_assert(SMEM <= 160 * 1024, "LDS budget");
+  // persistent kernel: the ring + the row-partial side area (E never staged in LDS)
+  constexpr int SMEM_P = 2 * (BM + BN) * ROWB + 2 * 8 * (BM / 2) * 4 + BM * 4;
+  static_assert(SMEM_P <= 160 * 1024, "LDS budget");
   auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>;
+  auto kernp = lmhead_fwd_persist_kernel<T>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)kernp, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_P);
     attr = true;
   }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const int grid = ntm * ntn;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
-                     (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
+  const char* pe = getenv("MIFT_LM_PERSIST");  // read per call: A/B-able within one process
+  const bool persist = (pe ? atoi(pe) != 0 : true) && K / BK >= 2;
+  if (persist) {
+    const int G = std::min(grid, num_cus());  // one 512-thread, 137 KiB block per CU
+    hipLaunchKernelGGL(kernp, dim3(G), dim3(512), SMEM_P, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
+                       (T*)E.data_ptr(), M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep.lm, grid, ep.group_m);
+  } else {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
+                       (T*)E.data_ptr(), nullptr, nullptr, M, N, K, (int)a.stride(0), (int)w.stride(0), N, ep, sk);
+  }
   // ~4 blocks per CU (2 rows per wave at distilgpt2's M = 8192): the rows of a wave are a dependent
   // chain of stats loads, so fewer, fatter blocks ran slower (512 blocks of 4 rows per wave: 19 us vs
   // 9.4 us for one row per wave), while the two-level arrival counters keep 1024 arrivals cheap

@@ -129,6 +129,9 @@ class _DecodeGraph:
 
     def __init__(self, model, B, S0, max_new, padded, pad, eos, fill, H, hd, dtype, dev):
         self.key = (B, S0, max_new, padded, pad, eos, fill)
+        # the graph holds raw pointers to the model's weights: keep the model alive so its id() (part of
+        # the cache key) cannot be reused by a rebuilt model whose weights live elsewhere
+        self.model = model
         L = len(model.blocks())
         self.cache = KVCache(L, B, H, S0 + max_new, hd, dtype, dev)
         self.B, self.S0, self.H, self.hd, self.fill, self.pad, self.eos = B, S0, H, hd, fill, pad, eos
@@ -164,6 +167,12 @@ class _DecodeGraph:
             self.step(model)  # eager warm-up (first launch of every kernel module), then capture
             i = 1
             if nsteps > 1:
+                # the capture must rebuild every cached LoRA operand pack INSIDE the graph (each replay then
+                # re-packs from the live adapter weights); without this the eager step's packs, built at the
+                # same arena version, are baked in and a later prefill that replaces them leaves the replays
+                # reading freed memory
+                from ..ops.fused import invalidate_packs
+                invalidate_packs(model)
                 g = torch.cuda.CUDAGraph()
                 was = gc.isenabled()
                 gc.collect()
@@ -182,8 +191,19 @@ class _DecodeGraph:
 _GRAPHS = {}
 
 
+def _arena_version(model):
+    """Version of the model's LoRA arena (bumped by every optimizer step / load), None without one."""
+    for m in model.modules():
+        a = getattr(m, "_arena", None)
+        if a is not None:
+            return (id(a), a.version)
+    return None
+
+
 def _decode_graph(model, key_args):
-    key = (id(model),) + tuple(key_args[:10])
+    # keyed by the adapter weights' version too: a graph captured before an optimizer step is not reused
+    # after it (its packs are rebuilt per replay, but the key keeps the contract explicit and cheap)
+    key = (id(model), _arena_version(model)) + tuple(key_args[:10])
     g = _GRAPHS.get(key)
     if g is None:
         if len(_GRAPHS) >= 4:

@@ -174,7 +174,7 @@ def replica_checksum(tensors):
 
 
 @torch.no_grad()
-def verify_replicas(tensors, group=None, rtol=0.0, resync=False):
+def verify_replicas(tensors, group=None, rtol=0.0, resync=False, slices=None, companions=None):
     """Checksum every tensor across the group; True when all replicas are bit-identical.
 
     Replaces DDP's construction-time broadcast: identical init by seed, verified with one
@@ -185,10 +185,15 @@ def verify_replicas(tensors, group=None, rtol=0.0, resync=False):
     all-reduce compute each output element once and forward it, so they do; a one-shot / low-latency
     algorithm that RCCL may select for a small bucket (distilgpt2's 1.6 MB of LoRA grads) sums the
     peers' inputs on every rank, and nothing guarantees the same summation order on every rank.
-    With ``rtol > 0`` a checksum mismatch is therefore measured instead of raised: the element-wise
-    spread (max - min over ranks) within ``rtol`` x the tensor's largest magnitude is an ulp-level
-    replica drift — reported, and with ``resync`` healed by broadcasting the group's first rank —
-    while a larger spread (real divergence: a lost update, a skipped step on one rank) raises."""
+    With ``rtol > 0`` a checksum mismatch is therefore measured instead of raised: within each
+    parameter slice (``slices[i]``: the (offset, numel) segments of tensor i, e.g. the LoRA arena's
+    per-parameter views; default: the whole tensor) the element-wise spread (max - min over ranks)
+    relative to the SLICE's largest magnitude — a small-magnitude parameter such as LoRA B early in
+    training is judged against its own scale, not the arena's — within ``rtol`` is an
+    ulp-level replica drift: reported, and with ``resync`` healed by broadcasting the group's first
+    rank's tensor together with its ``companions[i]`` (tensors of the same layout that evolve with
+    it, e.g. the AdamW moments, so the healed replicas keep identical optimizer state); a larger
+    spread (a lost update, a skipped step on one rank) raises."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return True
     cs = replica_checksum(tensors)
@@ -202,16 +207,22 @@ def verify_replicas(tensors, group=None, rtol=0.0, resync=False):
         raise RuntimeError(f"replica divergence detected: {len(bad)} tensor(s) differ, first index {bad[0]}")
     worst = 0.0
     for i in bad:
-        t = tensors[i].detach()
+        t = tensors[i].detach().reshape(-1)
         hi, lo = t.float().clone(), t.float().clone()
         dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
         dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
-        scale = float(torch.maximum(hi.abs().max(), lo.abs().max()))
-        rel = float((hi - lo).max()) / max(scale, 1e-30)
-        worst = max(worst, rel)
-        if rel > rtol:
-            raise RuntimeError(f"replica divergence detected: tensor {i} spread {rel:.3e} of its scale "
-                               f"(> rtol {rtol:g})")
+        segs = (slices[i] if slices is not None and slices[i] else None) or [(0, t.numel())]
+        for off, n in segs:
+            h, l_ = hi[off:off + n], lo[off:off + n]
+            d = float((h - l_).max()) if n else 0.0
+            if d == 0.0:
+                continue
+            scale = float(torch.maximum(h.abs().max(), l_.abs().max()))
+            rel = d / max(scale, 1e-30)
+            worst = max(worst, rel)
+            if rel > rtol:
+                raise RuntimeError(f"replica divergence detected: tensor {i} slice [{off}, {off + n}) spread "
+                                   f"{rel:.3e} of its scale (> rtol {rtol:g})")
     first = dist.get_global_rank(group, 0) if group is not None else 0
     if dist.get_rank() == first:
         print(f"[DDP] replica drift {worst:.3e} (<= rtol {rtol:g}) in {len(bad)} tensor(s)"
@@ -219,4 +230,6 @@ def verify_replicas(tensors, group=None, rtol=0.0, resync=False):
     if resync:
         for i in bad:
             dist.broadcast(tensors[i], src=first, group=group)
+            for c in (companions[i] if companions is not None and companions[i] else ()):
+                dist.broadcast(c, src=first, group=group)
     return False

@@ -183,37 +183,48 @@ def build_grid(ctx: DistContext, pp: int, virtual: int = 1):
     ctx.dp, ctx.pp = dp, pp
     ctx.pp_virtual = virtual if pp > 1 else 1
     ctx.dp_rank, ctx.pp_rank = ctx.rank // pp, ctx.rank % pp
+    # only the p2p communicators the selected layout uses are created: under RCCL with a bound
+    # device_id every group is a live communicator with its own buffers and streams
+    mode = os.environ.get("MIFT_PP_P2P", "link")
+    if mode not in ("link", "shared", "blocking"):
+        raise ValueError(f"MIFT_PP_P2P={mode!r}: link | shared | blocking")
+    ctx.p2p_mode = mode
+    ctx.n_groups = 0
+
+    def new_group(ranks):
+        ctx.n_groups += 1
+        return dist.new_group(ranks, timeout=ctx.timeout)
+
     # every rank must create every group in the same order
     for r in range(dp):
         ranks = list(range(r * pp, (r + 1) * pp))
         multi = pp > 1 and world > 1
-        g = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
-        # replica-wide p2p communicators per direction (the round-2 layout, MIFT_PP_P2P=shared)
-        gf = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
-        gb = dist.new_group(ranks, timeout=ctx.timeout) if multi else None
+        g = new_group(ranks) if multi else None  # grad-norm / found-inf / loss reductions over the pipe
         if ctx.rank in ranks:
             ctx.pp_group, ctx.pp_ranks = g, ranks
-            ctx.pp_fwd_group, ctx.pp_bwd_group = gf, gb
-        # per-link communicators (default): stage s's "recv from s-1" and "send to s+1" are on
+        if multi and mode == "shared":
+            # replica-wide p2p communicators per direction (the round-2 layout)
+            gf, gb = new_group(ranks), new_group(ranks)
+            if ctx.rank in ranks:
+                ctx.pp_fwd_group, ctx.pp_bwd_group = gf, gb
+        # per-link communicators (link / blocking): stage s's "recv from s-1" and "send to s+1" are on
         # different communicators, hence different RCCL streams, so neither ever queues behind the
         # other (pipeline.py, "p2p ordering")
-        for s in range(pp - 1) if multi else ():
+        for s in range(pp - 1) if (multi and mode != "shared") else ():
             pair = [ranks[s], ranks[s + 1]]
-            lf = dist.new_group(pair, timeout=ctx.timeout)
-            lb = dist.new_group(pair, timeout=ctx.timeout)
+            lf, lb = new_group(pair), new_group(pair)
             if ctx.rank == pair[0]:
                 ctx.link_f[1], ctx.link_b[1] = lf, lb
             elif ctx.rank == pair[1]:
                 ctx.link_f[0], ctx.link_b[0] = lf, lb
         if multi and ctx.pp_virtual > 1:
             pair = [ranks[0], ranks[-1]]
-            wf = dist.new_group(pair, timeout=ctx.timeout)
-            wb = dist.new_group(pair, timeout=ctx.timeout)
+            wf, wb = new_group(pair), new_group(pair)
             if ctx.rank in pair:
                 ctx.wrap_f, ctx.wrap_b = wf, wb
     for s in range(pp):
         ranks = list(range(s, world, pp))
-        g = dist.new_group(ranks, timeout=ctx.timeout) if dp > 1 and world > 1 else None
+        g = new_group(ranks) if dp > 1 and world > 1 else None
         if ctx.rank in ranks:
             ctx.dp_group, ctx.dp_ranks = g, ranks
     if ctx.dp_group is None and dp == 1 and world == 1:

@@ -238,7 +238,6 @@ class PipelineEngine:
             if len(getattr(model, "chunk_ranges", [])) != self.V:
                 raise ValueError(f"interleaved pipeline: the stage model holds "
                                  f"{len(getattr(model, 'chunk_ranges', []))} chunks, expected {self.V}")
-            graph = False  # the interleaved schedule runs eagerly
         self.dtype, self.d = act_dtype, hidden_size
         self.device = ctx.device
         self.stats = {"fwd": 0, "bwd": 0, "replays": 0}
@@ -292,7 +291,8 @@ class PipelineEngine:
         stream behind the transfer, so the host never blocks and xGMI transfers overlap the
         forward / backward kernels."""
         if self.V > 1:
-            return self._schedule_interleaved(mbs, gscale, micro_step0)
+            run = self.graphs.runner(mbs, gscale, micro_step0) if self.graphs is not None else None
+            return self._schedule_interleaved(mbs, run or _EagerChunkRun(self, mbs, gscale, micro_step0))
         if self.graphs is not None:
             run = self.graphs.runner(mbs, gscale, micro_step0)
             if run is not None:
@@ -300,13 +300,19 @@ class PipelineEngine:
         return self._schedule(mbs, _EagerRun(self, mbs, gscale, micro_step0))
 
     # ---- interleaved 1F1B (V model chunks per rank) ----
-    def _schedule_interleaved(self, mbs, gscale, micro_step0):
+    def _schedule_interleaved(self, mbs, run):
+        """Rank s's op list of ``schedule_interleaved``.  Receives are posted one op ahead of their
+        consumer (just in time under ``MIFT_PP_P2P=blocking``, whose ``_post`` waits on every receive:
+        a prefetch there would block on op j+1's input before op j's output is sent — with S = 2,
+        V = 2, M = 2 rank 0 would wait for the wrap-around activation of F(1, 0) before running F(0, 1),
+        which rank 1 needs first: ADVICE r4).  ``run`` is the eager (``_EagerChunkRun``) or the
+        replayed (``_ChunkGraphRun``) compute of one (chunk, micro-batch)."""
         S, s, V, M = self.S, self.s, self.V, len(mbs)
         ops = schedule_interleaved(S, s, M, V)
         nvs = S * V
         m = self.model
-        loss = torch.zeros((), dtype=torch.float32, device=self.device) if self.last else None
-        live, posted, sends = {}, {}, []
+        posted, sends = {}, []
+        pre = not self.blocking
 
         def vstage(c):
             return c * S + s
@@ -324,55 +330,53 @@ class PipelineEngine:
 
         def post(key):
             op, c, i = key
-            buf = torch.empty(self._act_shape(mbs[i]), dtype=self.dtype, device=self.device)
             if op == "F":  # activation of virtual stage vs - 1
+                buf, slot = run.x_buffer(c, i)
                 p2p, src = (self.rx_f, self.prev) if s > 0 else (self.rx_wf, self.last_rank)
             else:          # gradient from virtual stage vs + 1
+                buf, slot = run.g_buffer(c, i)
                 p2p, src = (self.rx_b, self.next) if s < S - 1 else (self.rx_wb, self.first_rank)
-            posted[key] = (self._post(p2p, recvs=[(buf, src)]), buf)
+            posted[key] = (self._post(p2p, recvs=[(buf, src)]), slot)
 
         def take(key):
             if key not in posted:
                 post(key)
-            pend, buf = posted.pop(key)
+            pend, slot = posted.pop(key)
             pend.wait()
-            return buf
+            return slot
 
         try:
             for j, (op, c, i) in enumerate(ops):
                 key = needs_recv(j)
                 if key is not None and key not in posted:
                     post(key)
-                nxt = needs_recv(j + 1)  # one op of receive prefetch
-                if nxt is not None and nxt not in posted:
-                    post(nxt)
+                if pre:
+                    nxt = needs_recv(j + 1)  # one op of receive prefetch
+                    if nxt is not None and nxt not in posted:
+                        post(nxt)
                 vs = vstage(c)
                 m.active_chunk = c
                 if op == "F":
-                    x = take(("F", c, i)).requires_grad_(True) if vs > 0 else None
-                    y = self._forward(mbs[i], x, micro_step0 + i)
-                    if vs == nvs - 1:
-                        loss.add_(y.detach())
-                    else:
+                    xslot = take(("F", c, i)) if vs > 0 else None
+                    y = run.forward(c, i, xslot)
+                    if vs < nvs - 1:
                         p2p, dst = (self.tx_f, self.next) if s < S - 1 else (self.tx_wf, self.first_rank)
-                        sends.append(self._post(p2p, sends=[(y.detach(), dst)]))
-                    live[(c, i)] = (x, y)
+                        sends.append(run.send_y(c, i, self._post(p2p, sends=[(y.detach(), dst)])))
                 else:
-                    x, y = live.pop((c, i))
-                    g = take(("B", c, i)) if vs < nvs - 1 else None
-                    if vs == nvs - 1:
-                        (y * gscale).backward()
-                    else:
-                        torch.autograd.backward(y, grad_tensors=g)
-                    self.stats["bwd"] += 1
+                    gslot = take(("B", c, i)) if vs < nvs - 1 else None
+                    gx = run.backward(c, i, gslot)
+                    if gslot is not None:
+                        run.release_g(c, i, gslot)
                     if vs > 0:
                         p2p, dst = (self.tx_b, self.prev) if s > 0 else (self.tx_wb, self.last_rank)
-                        sends.append(self._post(p2p, sends=[(x.grad, dst)]))
+                        sends.append(run.send_gx(c, i, self._post(p2p, sends=[(gx, dst)])))
+                    run.release_x(c, i)
         finally:
             m.active_chunk = None
         for p in sends:
-            p.wait()
-        return loss
+            if p is not None:
+                p.wait()
+        return run.finish()
 
     def _schedule(self, mbs, run):
         M = len(mbs)
@@ -497,6 +501,82 @@ class _EagerRun:
         return self.loss
 
 
+class _EagerChunkRun:
+    """Eager compute of one interleaved ``train_batch``: a fresh receive buffer per message (the
+    interleaved in-flight set has no ring bound to check), autograd graphs kept per (chunk, micro-batch)."""
+
+    def __init__(self, eng, mbs, gscale, micro_step0):
+        self.e, self.mbs, self.gscale, self.ms0 = eng, mbs, gscale, micro_step0
+        self.nvs = eng.S * eng.V
+        self.loss = torch.zeros((), dtype=torch.float32, device=eng.device) if eng.last else None
+        self.live = {}
+
+    def _last(self, c):
+        return c * self.e.S + self.e.s == self.nvs - 1
+
+    def x_buffer(self, c, i):
+        buf = torch.empty(self.e._act_shape(self.mbs[i]), dtype=self.e.dtype, device=self.e.device)
+        return buf, buf
+
+    g_buffer = x_buffer
+
+    def forward(self, c, i, x):
+        if x is not None:
+            x = x.requires_grad_(True)
+        y = self.e._forward(self.mbs[i], x, self.ms0 + i)
+        if self._last(c):
+            self.loss.add_(y.detach())
+        self.live[(c, i)] = (x, y)
+        return y
+
+    def backward(self, c, i, g):
+        x, y = self.live.pop((c, i))
+        if self._last(c):
+            (y * self.gscale).backward()
+        else:
+            torch.autograd.backward(y, grad_tensors=g)
+        self.e.stats["bwd"] += 1
+        return x.grad if x is not None else None
+
+    def send_y(self, c, i, pend):
+        return pend
+
+    send_gx = send_y
+
+    def release_x(self, c, i):
+        pass
+
+    def release_g(self, c, i, slot):
+        pass
+
+    def finish(self):
+        return self.loss
+
+
+def chunk_slot_counts(S, s, M, V, prefetch=True):
+    """Graph slots per model chunk on rank s of the interleaved schedule: the most micro-batches of
+    chunk c in flight at once, from the post of the receive feeding F(c, i) (at the top of the op
+    before it when receives are prefetched; F itself on the first virtual stage, which receives
+    nothing) until B(c, i) has been queued.  Per chunk the forwards and the backwards both run in
+    micro-batch order, so the in-flight set is a run of consecutive micro-batches and slot i % K_c is
+    never handed to micro-batch i + K_c before B(c, i) — the condition RCCL needs for a receive into
+    a reused buffer (``_Ring``)."""
+    ops = schedule_interleaved(S, s, M, V)
+    occ = [set() for _ in range(V)]
+    K = [1] * V
+    for j, (op, c, i) in enumerate(ops):
+        for jj in ((j, j + 1) if prefetch else (j,)):
+            if jj < len(ops) and ops[jj][0] == "F":
+                occ[ops[jj][1]].add(ops[jj][2])
+        for cc in range(V):
+            if occ[cc]:
+                assert max(occ[cc]) - min(occ[cc]) + 1 == len(occ[cc]), "in-flight set not consecutive"
+            K[cc] = max(K[cc], len(occ[cc]))
+        if op == "B":
+            occ[c].discard(i)
+    return K
+
+
 class _Ring:
     """Receive buffers reused round-robin per shape (``n`` slots: the in-flight bound).
 
@@ -568,63 +648,106 @@ class _StageGraphs:
                 return None  # eager warm-up step for this shape; capture on the next one
             while len(self.sets) >= self.max_sets:
                 self.sets.popitem(last=False)  # least recently used signature
-            slots = self._capture(mbs)
+            slots = self._capture(mbs) if self.e.V == 1 else self._capture_chunks(mbs)
             self.sets[sig] = slots
         self.sets.move_to_end(sig)
+        if self.e.V > 1:
+            return _ChunkGraphRun(self, slots, mbs, gscale, micro_step0)
         return _GraphRun(self, slots, mbs, gscale, micro_step0)
 
-    def _capture(self, mbs):
-        from ..models.layers import graph_seeds
+    def _capture_slot(self, mbs, first, last, pack):
+        """Forward + backward graphs of one slot (private pool).  ``first``: no received activation
+        (the embedding runs here); ``last``: the loss head runs here (seeded by ``self.gs``);
+        ``pack``: this capture rebuilds the per-step LoRA operand packs (the step's first replay)."""
         from ..ops import streams
         from ..ops.dispatch import C
         from ..ops.fused import invalidate_packs
         e = self.e
-        K = e.K
-        slots = []
+        sl = {"inp": {key: torch.empty_like(v) for key, v in mbs[0].items()},
+              "step": torch.zeros(1, dtype=torch.int64, device=e.device),
+              "send_y": None, "send_gx": None}
+        for key, v in mbs[0].items():
+            sl["inp"][key].copy_(v)
+        if not first:
+            sl["x"] = torch.zeros(e._act_shape(mbs[0]), dtype=e.dtype, device=e.device).requires_grad_(True)
+        if not last:
+            sl["g"] = torch.zeros(e._act_shape(mbs[0]), dtype=e.dtype, device=e.device)
+        if pack:
+            invalidate_packs(e.model)
+        C().set_seed_step(sl["step"])
+        gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        gc_was = gc.isenabled()
+        gc.collect()
+        gc.disable()  # no collection inside the captures (see train/graph.py)
+        try:
+            with torch.cuda.graph(gf, capture_error_mode="thread_local"):
+                y = e._forward(sl["inp"], sl.get("x"), 0)
+            with torch.cuda.graph(gb, pool=gf.pool(), capture_error_mode="thread_local"):
+                if last:
+                    (y * self.gs).backward(retain_graph=True)
+                else:
+                    torch.autograd.backward(y, grad_tensors=sl["g"], retain_graph=True)
+                streams.join()
+        finally:
+            if gc_was:
+                gc.enable()
+        C().set_seed_step(None)
+        sl.update(gf=gf, gb=gb, y=y, gx=(sl["x"].grad if not first else None))
+        return sl
+
+    def _captured(self, body):
+        from ..models.layers import graph_seeds
+        from ..ops import streams
+        from ..ops.dispatch import C
+        e = self.e
         torch.cuda.synchronize(e.device)
+        gc.collect()
+        torch.cuda.empty_cache()  # the eager warm-up's cached blocks: the slot pools are allocated next
         graph_seeds(True)
         streams.set_enabled(False)
         try:
-            for k in range(K):
-                sl = {"inp": {key: torch.empty_like(v) for key, v in mbs[0].items()},
-                      "step": torch.zeros(1, dtype=torch.int64, device=e.device),
-                      "send_y": None, "send_gx": None}
-                for key, v in mbs[0].items():
-                    sl["inp"][key].copy_(v)
-                if not e.first:
-                    sl["x"] = torch.zeros(e._act_shape(mbs[0]), dtype=e.dtype, device=e.device).requires_grad_(True)
-                if not e.last:
-                    sl["g"] = torch.zeros(e._act_shape(mbs[0]), dtype=e.dtype, device=e.device)
-                if k == 0:  # the per-step LoRA operand pack is captured into slot 0's forward
-                    invalidate_packs(e.model)
-                C().set_seed_step(sl["step"])
-                gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                gc_was = gc.isenabled()
-                gc.collect()
-                gc.disable()  # no collection inside the captures (see train/graph.py)
-                try:
-                    with torch.cuda.graph(gf, capture_error_mode="thread_local"):
-                        y = e._forward(sl["inp"], sl.get("x"), 0)
-                    with torch.cuda.graph(gb, pool=gf.pool(), capture_error_mode="thread_local"):
-                        if e.last:
-                            (y * self.gs).backward(retain_graph=True)
-                        else:
-                            torch.autograd.backward(y, grad_tensors=sl["g"], retain_graph=True)
-                        streams.join()
-                finally:
-                    if gc_was:
-                        gc.enable()
-                C().set_seed_step(None)
-                sl.update(gf=gf, gb=gb, y=y, gx=(sl["x"].grad if not e.first else None))
-                slots.append(sl)
+            return body()
         finally:
             graph_seeds(False)
             streams.set_enabled(None)
             C().set_seed_step(None)
-        e.stats["fwd"] -= K  # the captures ran _forward once per slot (backward bypassed _backward)
-        e.stats["captures"] = e.stats.get("captures", 0) + 1
-        torch.cuda.synchronize(e.device)
-        return slots
+            e.stats["captures"] = e.stats.get("captures", 0) + 1
+            torch.cuda.synchronize(e.device)
+
+    def _capture(self, mbs):
+        e = self.e
+
+        def body():
+            # the per-step LoRA operand pack is captured into slot 0's forward (the step's first replay)
+            slots = [self._capture_slot(mbs, e.first, e.last, pack=(k == 0)) for k in range(e.K)]
+            e.stats["fwd"] -= e.K  # the captures ran _forward once per slot (backward bypassed _backward)
+            return slots
+
+        return self._captured(body)
+
+    def _capture_chunks(self, mbs):
+        """Interleaved schedule: slots per (chunk, micro-batch mod K_c) (``chunk_slot_counts``), each
+        with its own pool.  Every rank's first op is F(0, 0), so slot (0, 0)'s forward carries the LoRA
+        operand packs; chunk c's multi-adapter packs are rebuilt inside its slot 0 (its first replay
+        of every step), which the chunk's later slots then read."""
+        e = self.e
+        Ks = chunk_slot_counts(e.S, e.s, len(mbs), e.V, prefetch=not e.blocking)
+        nvs = e.S * e.V
+
+        def body():
+            slots = []
+            try:
+                for c in range(e.V):
+                    vs = c * e.S + e.s
+                    e.model.active_chunk = c
+                    slots.append([self._capture_slot(mbs, vs == 0, vs == nvs - 1, pack=(c == 0 and k == 0))
+                                  for k in range(Ks[c])])
+            finally:
+                e.model.active_chunk = None
+            e.stats["fwd"] -= sum(Ks)
+            return slots
+
+        return self._captured(body)
 
 
 class _GraphRun:
@@ -710,6 +833,89 @@ class _GraphRun:
                 if sl[key] is not None:
                     sl[key].wait()
                     sl[key] = None
+        return self.loss
+
+
+class _ChunkGraphRun:
+    """Replay-based compute of one interleaved ``train_batch``: micro-batch i of chunk c replays
+    slot (c, i mod K_c); a slot's static output (y, or dX) is rewritten only after the send that
+    read it completed, a slot is handed to a new micro-batch only after the old one's backward was
+    queued (raises otherwise)."""
+
+    def __init__(self, gr, slots, mbs, gscale, micro_step0):
+        self.gr, self.e, self.mbs = gr, gr.e, mbs
+        self.slots = slots
+        self.nvs = self.e.S * self.e.V
+        gr.gs.copy_(gscale.reshape(()))
+        self.steps = torch.arange(micro_step0, micro_step0 + len(mbs), dtype=torch.int64).to(
+            self.e.device, non_blocking=True)
+        self.loss = torch.zeros((), dtype=torch.float32, device=self.e.device) if self.e.last else None
+        self.owner = [[None] * len(sl) for sl in slots]  # micro-batch holding each slot
+
+    def _k(self, c, i):
+        return i % len(self.slots[c])
+
+    def _claim(self, c, i):
+        k = self._k(c, i)
+        o = self.owner[c][k]
+        if o is not None and o != i:
+            raise RuntimeError(f"pipeline chunk {c} slot {k} reused by micro-batch {i} before the backward "
+                               f"of micro-batch {o} was queued")
+        self.owner[c][k] = i
+        return self.slots[c][k]
+
+    def x_buffer(self, c, i):
+        return self._claim(c, i)["x"].detach(), self._k(c, i)
+
+    def g_buffer(self, c, i):
+        return self._claim(c, i)["g"], self._k(c, i)
+
+    def forward(self, c, i, xslot):
+        sl = self._claim(c, i)
+        if sl["send_y"] is not None:
+            sl["send_y"].wait()  # the previous occupant's output has left before the replay rewrites it
+            sl["send_y"] = None
+        for key, v in self.mbs[i].items():
+            sl["inp"][key].copy_(v, non_blocking=True)
+        sl["step"].copy_(self.steps[i:i + 1])
+        sl["gf"].replay()
+        self.e.stats["replays"] += 1
+        self.e.stats["fwd"] += 1
+        if c * self.e.S + self.e.s == self.nvs - 1:
+            self.loss.add_(sl["y"].detach())
+        return sl["y"]
+
+    def backward(self, c, i, g):
+        sl = self._claim(c, i)
+        if sl["send_gx"] is not None:
+            sl["send_gx"].wait()
+            sl["send_gx"] = None
+        sl["gb"].replay()
+        self.e.stats["replays"] += 1
+        self.e.stats["bwd"] += 1
+        return sl["gx"]
+
+    def send_y(self, c, i, pend):
+        self.slots[c][self._k(c, i)]["send_y"] = pend
+        return None
+
+    def send_gx(self, c, i, pend):
+        self.slots[c][self._k(c, i)]["send_gx"] = pend
+        return None
+
+    def release_x(self, c, i):
+        self.owner[c][self._k(c, i)] = None
+
+    def release_g(self, c, i, slot):
+        pass  # the gradient buffer lives in the slot, freed with it by release_x
+
+    def finish(self):
+        for chunk in self.slots:
+            for sl in chunk:
+                for key in ("send_y", "send_gx"):
+                    if sl[key] is not None:
+                        sl[key].wait()
+                        sl[key] = None
         return self.loss
 
 

@@ -90,7 +90,8 @@ def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_
         step ≈ m·max_rank_units·u + (S − 1)·max_chunk_units·u + m·V·op_overhead + hops
     (the steady state runs at the slowest rank; warm-up and cool-down traverse the pipeline one
     chunk at a time).  ``op_overhead``: fixed cost per chunk-micro-batch (fwd + bwd): p2p latency and
-    host launches — 20 µs graph-replayed (V = 1), 60 µs eager (V > 1)."""
+    host launches — 20 µs graph-replayed (both schedules replay per-slot stage graphs since round 5),
+    60 µs eager."""
     from .pipeline import partition_layers
     name = name or getattr(cfg, "name_or_path", None) or "opt-2.7b"
     L = cfg.num_layers() if hasattr(cfg, "num_layers") else cfg.num_hidden_layers
@@ -105,12 +106,12 @@ def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_
     rank_units = [sum(units[c * stages + r] for c in range(v)) for r in range(stages)]
     seq_ms = cost_per_seq_ms(name, mb, measured)          # whole model, dp1, per sequence
     u = seq_ms * 1e-3 * mb / (L + head_layers)             # s per layer-equivalent per micro-batch
-    ovh = op_overhead_s if op_overhead_s is not None else (20e-6 if v == 1 else 60e-6)
+    ovh = op_overhead_s if op_overhead_s is not None else 20e-6
     hop = mb * seq * d * dtype_bytes / LINK_BW + LINK_LAT
     step = (m * max(rank_units) + (stages - 1) * max(units)) * u + m * v * ovh + 2 * (nvs - 1) / stages * hop
     best_dp1 = min(cost_per_seq_ms(name, x, measured) for x in _divisors(per_replica))
     dp1_step_per_gpu = best_dp1 * 1e-3 * per_replica / stages   # same work on S GPUs without a bubble
-    return {"micro_batch": mb, "micro_batches": m, "virtual": v, "split": list(split),
+    return {"micro_batch": mb, "micro_batches": m, "virtual": v, "split": list(split), "op_overhead_us": ovh * 1e6,
             "stage_ms": round(max(rank_units) * u * 1e3, 3), "hop_ms": round(hop * 1e3, 4),
             "step_ms": round(step * 1e3, 2), "bubble": round((stages - 1) / (v * m + stages - 1), 4),
             "efficiency_vs_dp1": round(dp1_step_per_gpu / step, 4)}
@@ -125,10 +126,26 @@ def act_bytes_per_token_layer(cfg, dtype_bytes=2):
     return (16 * d + 2 * ffn) * dtype_bytes
 
 
+def graph_slots(stages, micro_batches, virtual, rank=0):
+    """Chunk-micro-batches of saved activations one captured stage-graph set holds on ``rank``: the
+    per-slot graphs of parallel/pipeline.py (K = S − s + 1 slots for 1F1B, Σ_c K_c for the
+    interleaved schedule), each keeping one forward's activations in its private pool."""
+    if virtual <= 1:
+        return stages - rank + 1
+    from .pipeline import chunk_slot_counts
+    return sum(chunk_slot_counts(stages, rank, micro_batches, virtual))
+
+
 def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=288 * 10 ** 9,
-                       hbm_frac=0.85, measured=None, name=None, candidates=None, virtual=1):
+                       hbm_frac=0.85, measured=None, name=None, candidates=None, virtual=1, graph_sets=None):
     """The feasible micro-batch (divisor of ``per_replica``) with the shortest predicted step.
-    ``virtual``: model chunks per rank (int), or "auto" to choose among 1, 2, 4, ... as well."""
+    ``virtual``: model chunks per rank (int), or "auto" to choose among 1, 2, 4, ... as well.
+    Memory: rank 0's live activations at the end of the eager warm-up, or ``graph_sets`` captured
+    slot sets of stage graphs (``MIFT_PP_GRAPH_SETS``, default 2: the epoch's ragged last step keeps
+    its own set), whichever is larger (the eager step's cached blocks are released before a capture)."""
+    import os
+    if graph_sets is None:
+        graph_sets = int(os.environ.get("MIFT_PP_GRAPH_SETS", "2"))
     L = cfg.num_layers() if hasattr(cfg, "num_layers") else cfg.num_hidden_layers
     n_params = getattr(cfg, "num_params", None)
     d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd")
@@ -148,10 +165,12 @@ def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=2
             if v > 1 and m % stages:
                 continue
             inflight = stages if v == 1 else min(2 * (stages - 1) + (v - 1) * stages + 1, m * v)
-            need = inflight * mb * seq * per_tok      # rank 0's live activations at the end of warm-up
+            held = max(inflight, graph_sets * graph_slots(stages, m, v)) if stages > 1 else inflight
+            need = held * mb * seq * per_tok      # rank 0's live activations (eager warm-up or graph slots)
             p = predict(cfg, seq, per_replica, stages, mb, measured=measured, dtype_bytes=dtype_bytes, name=name,
                         virtual=v)
             p["act_gib"] = round(need / GiB, 2)
+            p["graph_slot_sets"] = graph_sets
             p["fits"] = need <= budget
             table.append(p)
             if p["fits"] and (best is None or p["step_ms"] < best["step_ms"] - 1e-9):

@@ -6,8 +6,8 @@ per step (tools/graph_overhead.py), 0.17 ms as a graph replay.  The eager
 step is therefore GPU-bound today, but the host cost becomes the limit as the
 kernels get faster, with more micro-batches per step, and for small decode
 steps.  ``GraphedStep`` captures the forward and
-backward of all micro-batches of a step — LoRA packing, fused kernels,
-hipBLASLt LM head — into ONE hipGraph and replays it: one host launch per
+backward of all micro-batches of a step — LoRA packing, fused kernels, the
+hand-written fused LM head + cross-entropy — into ONE hipGraph and replays it: one host launch per
 step and no inter-kernel gaps.  ``MIFT_GRAPH_SIDE=1`` also forks the LoRA
 weight-gradient kernels onto a side stream inside the graph (mift.ops.streams);
 measured on MI355X it slows the co-running dgrad GEMMs more than it hides

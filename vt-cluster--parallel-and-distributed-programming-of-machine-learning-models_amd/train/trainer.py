@@ -188,6 +188,14 @@ class Trainer:
             raise RuntimeError("graph=on needs the fused GPU LoRA path without recompute")
         return ok
 
+    def _replicated_opt_state(self):
+        """The optimizer tensors laid out like the full arena and identical on every DP replica (the
+        AdamW moments), resynchronised together with the parameters; ZeRO-1 shards them per rank."""
+        if self.cfg.zero_stage:
+            return []
+        return [t for t in (getattr(self.opt, "m", None), getattr(self.opt, "v", None))
+                if t is not None and t.numel() == self.arena.param.numel()]
+
     def _graph_ok(self):
         return self.pp == 1 and self._fused_graphable("step")
 
@@ -363,7 +371,9 @@ class Trainer:
                         print(lab_step_line(self.rank, self.global_step, dt * 1000, sps, sps * seq), flush=True)
                 self._tok_seen += sum(int(mb["input_ids"].numel()) for mb in mbs) * self.dp
                 if cfg.consistency_every and self.dp > 1 and self.global_step % cfg.consistency_every == 0:
-                    verify_replicas([self.arena.param], group=self.dp_group, rtol=cfg.consistency_rtol, resync=True)
+                    verify_replicas([self.arena.param], group=self.dp_group, rtol=cfg.consistency_rtol, resync=True,
+                                    slices=[[(o, p.numel()) for o, (_, p) in zip(self.arena.offsets, self.arena.named)]],
+                                    companions=[self._replicated_opt_state()])
                 if log_now:
                     self._perf_log(mbs)
                     st = self.opt.stats()
