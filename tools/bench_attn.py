@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="distilgpt2 shape over batch sizes (heads per CU: is the kernel per-CU-throughput or "
                          "latency bound, and does the 1.5-heads-per-CU imbalance at B = 32 cost time?)")
+    ap.add_argument("--ab", default=None, help="VAR=v0,v1: A/B the env var (arms interleaved per shape, "
+                                              "best of 3 alternations each)")
+    ap.add_argument("--only", default=None, help="comma list of shape names")
     a = ap.parse_args()
     C = mift._ext.require()
     rows = []
@@ -32,11 +35,36 @@ def main():
     if a.sweep:
         shapes = [(f"distilgpt2-B{b}-p{p}", b, 256, 12, 64, torch.bfloat16, p) for p in (0.0, 0.1)
                   for b in (8, 16, 21, 32, 43, 64)]
+    if a.only:
+        shapes = [x for x in shapes if x[0] in a.only.split(",")]
     for name, B, S, H, hd, dt, p in shapes:
         qkv = torch.randn(B * S, 3 * H * hd, device="cuda", dtype=dt)
         sc = hd ** -0.5
         o, lse = C.attn_fwd(qkv, B, S, H, hd, sc, p, 1, None)
         do = torch.randn_like(o)
+        if a.ab:
+            var, vals = a.ab.split("=")
+            res, outs = {}, {}
+            for _ in range(3):
+                for v in vals.split(","):
+                    os.environ[var] = v
+                    f = timeit(lambda: C.attn_fwd(qkv, B, S, H, hd, sc, p, 1, None))
+                    b = timeit(lambda: C.attn_bwd(do, qkv, o, lse, B, S, H, hd, sc, p, 1, None))
+                    r = res.setdefault(v, [9e9, 9e9])
+                    res[v] = [min(r[0], f), min(r[1], b)]
+                    outs[v] = (C.attn_fwd(qkv, B, S, H, hd, sc, p, 1, None)[0],
+                               C.attn_bwd(do, qkv, o, lse, B, S, H, hd, sc, p, 1, None))
+            os.environ.pop(var, None)
+            fl = 4.0 * B * H * S * S * hd / 2
+            row = {"name": name, "B": B, "S": S, "H": H, "hd": hd, "var": var}
+            v0 = vals.split(",")[0]
+            for v, (f, b) in res.items():
+                row[f"{v}_fwd_us"], row[f"{v}_bwd_us"] = round(f * 1e3, 1), round(b * 1e3, 1)
+                row[f"{v}_fwd_tflops"], row[f"{v}_bwd_tflops"] = round(fl / f / 1e9, 1), round(2.5 * fl / b / 1e9, 1)
+                row[f"{v}_same_as_{v0}"] = bool(torch.equal(outs[v][0], outs[v0][0]) and torch.equal(outs[v][1], outs[v0][1]))
+            print(json.dumps(row), flush=True)
+            rows.append(row)
+            continue
         tf = timeit(lambda: C.attn_fwd(qkv, B, S, H, hd, sc, p, 1, None))
         tb = timeit(lambda: C.attn_bwd(do, qkv, o, lse, B, S, H, hd, sc, p, 1, None))
         q, k, v = qkv.view(B, S, 3, H, hd).permute(2, 0, 3, 1, 4)

@@ -181,6 +181,22 @@ MIFT_HD void load_reg_frags(vec8<T>* f, const T* src, int64_t ld, int row, int n
   }
 }
 
+// Block -> (head, tile) for the tiled kernels: the tiles of one head share K/V (forward, dQ) or Q/dO
+// (dK/dV), re-read once per tile.  Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share
+// one), so consecutive block ids — one head's tiles — sat on 8 different L2s and every re-read went to
+// the Infinity Cache.  The bijective remap (gemm.hip, guide T1) gives each XCD a contiguous run of
+// block ids: a head's tiles run on one XCD and re-read its L2.  MIFT_ATTN_XCD=0: off (A/B).
+MIFT_HD int attn_block_id(int xcd_remap) {
+  const int b = blockIdx.x;
+  if (!xcd_remap) return b;
+  const int n = gridDim.x, q = n / 8, r = n % 8, xcd = b % 8, loc = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+inline int attn_xcd_env() {
+  const char* e = getenv("MIFT_ATTN_XCD");
+  return e ? atoi(e) : 1;
+}
+
 MIFT_HD bool drop_keep(uint64_t seed, uint32_t thr, int64_t bh, int S, int q, int k) {
   return mift_keep(seed, ((uint64_t)bh * S + q) * S + k, thr);
 }
@@ -194,11 +210,18 @@ MIFT_HD bool drop_keep(uint64_t seed, uint32_t thr, int64_t bh, int S, int q, in
 // MFMA and the K/V global->LDS traffic per query.  Groups whose 16 queries all
 // precede a key tile skip it (wave-uniform branch; same result as a fully
 // masked tile).
-template <typename T, int HD, int QG>
+// OT (output transposed, default): P·V is issued with the operands swapped, mfma(Vᵀ frag, P frag),
+// which computes Oᵀ: lane (g, qc) then holds hd columns 16i + 4g .. +3 of ITS OWN query qc instead of
+// one column of queries 4g .. 4g+3.  The softmax state (m, l, alpha) is per query = per lane already,
+// so the rescale and the final 1/l need no cross-lane shuffles, and the output leaves as one 8-B store
+// per 16 columns (NOT per lane) instead of 4·NOT 2-B stores — the attention store tail is issue-bound
+// (MI355X_MICROARCH.md constants: 16 dwordx2 per lane ≈ 9.3k cycles for the last-finishing half).
+template <typename T, int HD, int QG, bool OT = true>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ kv_len,
                                                        int B, int S, int H, float scale, uint64_t seed,
-                                                       const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
+                                                       const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep,
+                                                       int xcd) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   constexpr int BQB = BQ * QG;  // queries per block
@@ -209,8 +232,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, qc = lane & 15;
   const int nqt = (S + BQB - 1) / BQB;
-  const int qt = nqt - 1 - (blockIdx.x % nqt);  // heavy (late) query tiles first
-  const int bh = blockIdx.x / nqt;
+  const int bid = attn_block_id(xcd);
+  const int qt = nqt - 1 - (bid % nqt);  // heavy (late) query tiles first
+  const int bh = bid / nqt;
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
@@ -323,11 +347,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
       }
       l[j] = l[j] * alpha + psum;
       if (resc) {
+        if constexpr (OT) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float ar = __shfl(alpha, g * 4 + r, 64);
+          for (int i = 0; i < G::NOT; ++i) o[j][i] *= alpha;
+        } else {
 #pragma unroll
-          for (int i = 0; i < G::NOT; ++i) o[j][i][r] *= ar;
+          for (int r = 0; r < 4; ++r) {
+            const float ar = __shfl(alpha, g * 4 + r, 64);
+#pragma unroll
+            for (int i = 0; i < G::NOT; ++i) o[j][i][r] *= ar;
+          }
         }
       }
     }
@@ -338,7 +367,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
         const vec8<T> vf = tr_frag<T>(Vs, G::TRS, 32 * s2, i * 16, lane);
 #pragma unroll
         for (int j = 0; j < QG; ++j)
-          if (act[j]) o[j][i] = mfma16(pf[j][s2], vf, o[j][i]);
+          if (act[j]) o[j][i] = OT ? mfma16(vf, pf[j][s2], o[j][i]) : mfma16(pf[j][s2], vf, o[j][i]);
       }
   }
   T* Og = out + (int64_t)b * S * D + h * HD;
@@ -350,13 +379,25 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
     const float inv_l = lj > 0.f ? 1.f / lj : 0.f;
     const int q0j = q0 + 16 * j, myq = q0j + qc;
     if (g == 0 && myq < S) lse[(int64_t)bh * S + myq] = (lj > 0.f) ? (m[j] + log2f(lj)) * LN2 : -INFINITY;
+    if constexpr (OT) {
+      if (myq < S) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float il = __shfl(inv_l, g * 4 + r, 64);
-      const int q = q0j + g * 4 + r;
-      if (q < S) {
+        for (int i = 0; i < G::NOT; ++i) {
+          float v4[4];
 #pragma unroll
-        for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (T)(o[j][i][r] * il);
+          for (int r = 0; r < 4; ++r) v4[r] = o[j][i][r] * inv_l;
+          store4<T>(Og + (int64_t)myq * D + i * 16 + g * 4, v4);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float il = __shfl(inv_l, g * 4 + r, 64);
+        const int q = q0j + g * 4 + r;
+        if (q < S) {
+#pragma unroll
+          for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (T)(o[j][i][r] * il);
+        }
       }
     }
   }
@@ -447,7 +488,7 @@ int attn_seq_mode() {
   return e ? atoi(e) : 1;
 }
 
-template <typename T, int HD, int NW>
+template <typename T, int HD, int NW, bool OT = true>  // OT: see attn_fwd_kernel
 __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                               float* __restrict__ lse, const int* __restrict__ kv_len,
                                                               int B, int S, int H, float scale, uint64_t seed,
@@ -613,29 +654,49 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
       }
       l = l * alpha + psum;
       if (resc) {
+        if constexpr (OT) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float ar = __shfl(alpha, g * 4 + r, 64);
+          for (int i = 0; i < G::NOT; ++i) o[i] *= alpha;
+        } else {
 #pragma unroll
-          for (int i = 0; i < G::NOT; ++i) o[i][r] *= ar;
+          for (int r = 0; r < 4; ++r) {
+            const float ar = __shfl(alpha, g * 4 + r, 64);
+#pragma unroll
+            for (int i = 0; i < G::NOT; ++i) o[i][r] *= ar;
+          }
         }
       }
 #pragma unroll
       for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) o[i] = mfma16(pf[s2], tr_frag<T>(Vs, G::TRS, k0 + 32 * s2, i * 16, lane), o[i]);
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const vec8<T> vf = tr_frag<T>(Vs, G::TRS, k0 + 32 * s2, i * 16, lane);
+          o[i] = OT ? mfma16(vf, pf[s2], o[i]) : mfma16(pf[s2], vf, o[i]);
+        }
     }
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     const float inv_l = l > 0.f ? 1.f / l : 0.f;
     if (g == 0 && myq < S) lse[(int64_t)bh * S + myq] = (l > 0.f) ? (m + log2f(l)) * LN2 : -INFINITY;
+    if constexpr (OT) {
+      if (myq < S) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float il = __shfl(inv_l, g * 4 + r, 64);
-      const int q = q0 + g * 4 + r;
-      if (q < S) {
+        for (int i = 0; i < G::NOT; ++i) {
+          float v4[4];
 #pragma unroll
-        for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (T)(o[i][r] * il);
+          for (int r = 0; r < 4; ++r) v4[r] = o[i][r] * inv_l;
+          store4<T>(Og + (int64_t)myq * D + i * 16 + g * 4, v4);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float il = __shfl(inv_l, g * 4 + r, 64);
+        const int q = q0 + g * 4 + r;
+        if (q < S) {
+#pragma unroll
+          for (int i = 0; i < G::NOT; ++i) Og[(int64_t)q * D + i * 16 + qc] = (T)(o[i][r] * il);
+        }
       }
     }
   }
@@ -648,7 +709,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
                                                           float* __restrict__ Dv, T* __restrict__ dqkv,
                                                           const int* __restrict__ kv_len, int B, int S, int H,
                                                           float scale, uint64_t seed, const int64_t* __restrict__ sstep, uint32_t thr,
-                                                          float inv_keep) {
+                                                          float inv_keep, int xcd) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -659,8 +720,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, qc = lane & 15;
   const int nqt = (S + BQ - 1) / BQ;
-  const int qt = nqt - 1 - (blockIdx.x % nqt);
-  const int bh = blockIdx.x / nqt;
+  const int bid = attn_block_id(xcd);
+  const int qt = nqt - 1 - (bid % nqt);
+  const int bh = bid / nqt;
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
@@ -767,7 +829,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(const T* __rest
                                                             const float* __restrict__ lse, const float* __restrict__ Dv,
                                                             T* __restrict__ dqkv, const int* __restrict__ kv_len,
                                                             int B, int S, int H, float scale, uint64_t seed,
-                                                            const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep) {
+                                                            const int64_t* __restrict__ sstep, uint32_t thr, float inv_keep,
+                                                            int xcd) {
   seed = mift_seed(seed, sstep);
   using G = Geo<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -781,8 +844,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(const T* __rest
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
   const int g = lane >> 4, kc = lane & 15;
   const int nkt = (S + BKV - 1) / BKV;
-  const int kt = blockIdx.x % nkt;
-  const int bh = blockIdx.x / nkt;
+  const int bid = attn_block_id(xcd);
+  const int kt = bid % nkt;
+  const int bh = bid / nkt;
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
@@ -1306,8 +1370,9 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 2 : 1) void attn_fwd2_kernel(co
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, qi = lane & 31;
   const int nqt = (S + BQB - 1) / BQB;
-  const int qt = nqt - 1 - (blockIdx.x % nqt);  // heavy (late) query tiles first
-  const int bh = blockIdx.x / nqt;
+  const int bid = attn_block_id(0);
+  const int qt = nqt - 1 - (bid % nqt);  // heavy (late) query tiles first
+  const int bh = bid / nqt;
   const int b = bh / H, h = bh % H;
   const int D = H * HD;
   const int64_t ld = 3LL * D;
@@ -1534,11 +1599,19 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
                        seed, mift_seed_step(), thr, inv_keep, (seq && thr != 0) ? dmask : nullptr);
     return;
   }
+  // transposed-output P·V (read per call: A/B): on for the whole-sequence kernel (distilgpt2 fwd 23.3 ->
+  // 22.8 us), off for the tiled one (OPT-2.7B 49.2 vs 49.9 us, OPT-6.7B 115.9 vs 118.5;
+  // profiles/r5/bench_attn_ot_xcd.jsonl)
+  const char* ote = getenv("MIFT_ATTN_OT");
+  const bool ot = ote ? atoi(ote) != 0 : seq;
   if (seq) {
-    auto kern = attn_fwd_seq_kernel<T, HD, 8>;
+    auto kern = ot ? attn_fwd_seq_kernel<T, HD, 8, true> : attn_fwd_seq_kernel<T, HD, 8, false>;
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attn_fwd_seq_kernel<T, HD, 8, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)attn_fwd_seq_kernel<T, HD, 8, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       attr = true;
     }
     int nblk = B * H;
@@ -1552,12 +1625,13 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
     const int nqt = (S + 2 * BQ - 1) / (2 * BQ);
     hipLaunchKernelGGL((attn_fwd_kernel<T, HD, 2>), dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
                        (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr,
-                       inv_keep);
+                       inv_keep, attn_xcd_env());
   } else {
     const int nqt = (S + BQ - 1) / BQ;
-    hipLaunchKernelGGL((attn_fwd_kernel<T, HD, 1>), dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
+    auto k1 = ot ? attn_fwd_kernel<T, HD, 1, true> : attn_fwd_kernel<T, HD, 1, false>;
+    hipLaunchKernelGGL(k1, dim3(B * H * nqt), dim3(256), smem, st, (const T*)qkv.data_ptr(),
                        (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale, seed, mift_seed_step(), thr,
-                       inv_keep);
+                       inv_keep, attn_xcd_env());
   }
 }
 
@@ -1594,7 +1668,8 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
   const int smem_dq = 2 * G::ROW_BYTES + G::TR_BYTES;
   hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD>), dim3(B * H * nqt), dim3(256), smem_dq, st, (const T*)qkv.data_ptr(),
                      (const T*)o.data_ptr(), (const T*)dout.data_ptr(), lse.data_ptr<float>(),
-                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+                     Dv.data_ptr<float>(), (T*)dqkv.data_ptr(), kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep,
+                     attn_xcd_env());
   const int smem_kv = 2 * G::ROW_BYTES + 2 * G::TR_BYTES + 2 * 64 * 4;
   // minimum waves per SIMD of the tiled dK/dV kernel (MIFT_ATTN_DKDV_OCC, read per call: A/B).  With the
   // round-3 bound (HD <= 64 ? 3 : 1) hd 128 took 268 registers — one wave per SIMD, below the two its LDS
@@ -1605,7 +1680,7 @@ void bwd_launch(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor&
   auto kv = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(B * H * nkt), dim3(256), smem_kv, st, (const T*)qkv.data_ptr(),
                        (const T*)dout.data_ptr(), lse.data_ptr<float>(), Dv.data_ptr<float>(), (T*)dqkv.data_ptr(),
-                       kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep);
+                       kvl, B, S, H, scale, seed, mift_seed_step(), thr, inv_keep, attn_xcd_env());
   };
   if (occ == 2) kv(attn_bwd_dkdv_kernel<T, HD, 2>);
   else if (occ == 3) kv(attn_bwd_dkdv_kernel<T, HD, 3>);

@@ -1077,7 +1077,10 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* redm = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);  // [NW][WM] wave row maxima
   float* reds = redm + NW * WM;                                     // [NW][WM] wave row sums
-  int* labs = reinterpret_cast<int*>(reds + NW * WM);               // [BM] row targets
+  // raw label ids of rows m0 .. m0 + 383 (3 KiB: the unshifted ids need row + 1), brought in by LDS-DMA
+  // at the tile's first k-tile: a plain global load used in the epilogue would make hipcc wait
+  // vmcnt(0) there, draining the next tile's in-flight ring DMA (guide §5 "Pipelining across barriers")
+  int64_t* ids = reinterpret_cast<int64_t*>(reds + NW * WM);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / NWN, wn = wave % NWN;
@@ -1150,10 +1153,13 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
   auto epilogue = [&](int m0, int n0, auto fullc) {
     constexpr bool FULL = decltype(fullc)::value;
     const int V = lm.V;
-    if (tid < BM) {
-      const int64_t l = lm_label(lm.labels, min(m0 + tid, M - 1), lm.shift, lm.ignore);
-      labs[tid] = (l >= 0 && l < V) ? (int)l : -1;
-    }
+    // lm_label on the LDS copy of the ids (rows m0 + r, r < BM; the copy starts at row m0)
+    auto label_of = [&](int lrow) {
+      const int row = m0 + lrow;
+      if (row >= M) return -1;
+      const int64_t l = lm.shift <= 0 ? ids[lrow] : (row % lm.shift == lm.shift - 1) ? (int64_t)-1 : ids[lrow + 1];
+      return (l == lm.ignore || l < 0 || l >= V) ? -1 : (int)l;
+    };
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       float m = -INFINITY;
@@ -1176,7 +1182,7 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
       if (m == -INFINITY) m = 0.f;
       const int lrow = wm * WM + i * 16 + fr;
       const int row = m0 + lrow;
-      const int lab = labs[lrow];
+      const int lab = label_of(lrow);
       const float mb = m * L2E;
       float s = 0.f, zl = 0.f;
       bool hit = false;
@@ -1230,9 +1236,17 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
     }
   };
 
+  // waves 0-2: one 1-KiB LDS-DMA each of ids[m0 + 128w .. +127] (rows clamped in range)
+  auto stage_ids = [&](int m0) {
+    if (wave < 3) {
+      const int r = min(m0 + wave * 128 + lane * 2, M - 2);  // M even (host-checked): r even, 16-B aligned
+      __builtin_amdgcn_global_load_lds((const void*)(lm.labels + r), (void*)(ids + wave * 128), 16, 0, 0);
+    }
+  };
   int m0, n0, nm0 = 0, nn0 = 0;
   coords(0, m0, n0);
   if (ntl > 1) coords(1, nm0, nn0);
+  stage_ids(m0);
   stage_half(0, m0, n0, 0, 0, 0);
   stage_half(0, m0, n0, 0, 0, 1);
   stage_half(0, m0, n0, 0, 1, 0);
@@ -1249,11 +1263,15 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
   asm volatile("" ::: "memory");
   const int arow = wm * WM + fr, brow = wn * WN + fr;
   const int sw0 = (fq ^ (fr & 7)) << 4, sw1 = ((4 + fq) ^ (fr & 7)) << 4;
+  // early: the previous epilogue already issued this tile's k-tile 1 A halves (then FULL-tile epilogues
+  // leave 16 E stores per lane younger than them, which the first ph3 wait need not drain)
+  int early = 0;  // 0 none, 1 issued (wait conservatively), 2 issued behind a FULL epilogue's 16 stores
   for (int j = 0; j < ntl; ++j) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int q = 0; q < TN; ++q) acc[i][q] = float4_{0.f, 0.f, 0.f, 0.f};
+    if (j > 0) stage_ids(m0);  // older than every ring DMA waited for below: landed by the first ph3
     for (int kt = 0; kt < nk; ++kt) {
       const int g = j * nk + kt;
       const char* As = smem + (g & 1) * STAGE_BYTES;
@@ -1272,14 +1290,15 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
         bq[q][0] = rd(Bs + (brow + q * 16) * ROWB + sw0);
         bq[q][1] = rd(Bs + (brow + q * 16) * ROWB + sw1);
       }
-      if (g + 1 < total) stage_half((g + 1) & 1, m1, n1, k1, 0, 0);
+      const bool pre = kt == 0 && early != 0;  // block-uniform
+      if (g + 1 < total && !pre) stage_half((g + 1) & 1, m1, n1, k1, 0, 0);
       cluster(0, 0);
 #pragma unroll
       for (int q = 2; q < 4; ++q) {
         bq[q][0] = rd(Bs + (brow + q * 16) * ROWB + sw0);
         bq[q][1] = rd(Bs + (brow + q * 16) * ROWB + sw1);
       }
-      if (g + 1 < total) stage_half((g + 1) & 1, m1, n1, k1, 0, 1);
+      if (g + 1 < total && !pre) stage_half((g + 1) & 1, m1, n1, k1, 0, 1);
       cluster(0, 1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1290,7 +1309,10 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
       if (g + 2 < total) {
         stage_half(g & 1, m2, n2, k2, 1, 0);
         stage_half(g & 1, m2, n2, k2, 1, 1);
-        wait_vmcnt<4>();
+        // retire k-tile g+1 (A, B): all but the 4 B(g+2) pieces — and, right after a FULL epilogue that
+        // issued k-tile g+1's A early, all but those 4 and the 16 younger E stores per lane
+        if (kt == 0 && early == 2) wait_vmcnt<20>();
+        else wait_vmcnt<4>();
       } else {
         wait_vmcnt<0>();
       }
@@ -1298,8 +1320,23 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
     }
     if (wm == 0) __builtin_amdgcn_s_barrier();  // re-align the wave rows for the epilogue's barriers
     asm volatile("" ::: "memory");
-    if (n0 + BN <= lm.V && !(lm.dbg & 4)) epilogue(m0, n0, std::true_type{});  // block-uniform
+    // k-tile g+2 = the next tile's k-tile 1: its A halves go to the buffer whose A region every wave
+    // finished reading in the last k-tile's ph2 (before the barrier above) — issued now, ahead of the
+    // epilogue's stores, so the next tile's first ph3 wait does not also wait for those stores
+    {
+      const int g = j * nk + nk - 1;
+      early = 0;
+      if (g + 2 < total) {
+        const int k2 = 1 - (nk == 1);
+        stage_half(g & 1, nm0, nn0, k2, 0, 0);
+        stage_half(g & 1, nm0, nn0, k2, 0, 1);
+        early = 1;
+      }
+    }
+    const bool full = n0 + BN <= lm.V && !(lm.dbg & 4);  // block-uniform
+    if (full) epilogue(m0, n0, std::true_type{});
     else epilogue(m0, n0, std::false_type{});
+    if (early && full && !(lm.dbg & 1)) early = 2;
     if (wm == 1 && j + 1 < ntl) __builtin_amdgcn_s_barrier();  // re-stagger for the next tile
     asm volatile("" ::: "memory");
     m0 = nm0;
@@ -1976,15 +2013,20 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);
   if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   {
-    const char* g = getenv("MIFT_GEMM_GROUP");  // row-panel order measured best for the fused head
-    ep.group_m = g ? atoi(g) : 0;
+    // tile raster of the head: the 32 blocks an XCD runs at once cover g row panels x 32/g vocab tiles,
+    // so each W tile is fetched from the Infinity Cache once per g row panels (row-panel order, g = 1,
+    // fetched 2.5 GB per distilgpt2 forward: FETCH_SIZE, profiles/r5/pmc_roofline_distilgpt2_step.txt);
+    // persistent kernel measured g = 4 best at K = 768 (648 vs 714 us), g = 8 at K = 2560 (1381 vs 1491)
+    // (profiles/r5/bench_lm_persist.jsonl).  MIFT_LM_GROUP (per call) overrides.
+    const char* g = getenv("MIFT_LM_GROUP");
+    ep.group_m = g ? atoi(g) : (K <= 1024 ? 4 : 8);
   }
   SkArgs sk{};
   // staging ring (128 KiB) reused for the E tile + the two row-partial arrays
   constexpr int SMEM = std::max(2 * (BM + BN) * ROWB, BM * CTile<BN>::CLD * 2 + 2 * 8 * (BM / 2) * 4 + BM * 4);
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   // persistent kernel: the ring + the row-partial side area (E never staged in LDS)
-  constexpr int SMEM_P = 2 * (BM + BN) * ROWB + 2 * 8 * (BM / 2) * 4 + BM * 4;
+  constexpr int SMEM_P = 2 * (BM + BN) * ROWB + 2 * 8 * (BM / 2) * 4 + 384 * 8;  // + the ids copy
   static_assert(SMEM_P <= 160 * 1024, "LDS budget");
   auto kern = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 1>;
   auto kernp = lmhead_fwd_persist_kernel<T>;
@@ -1996,8 +2038,12 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   const int grid = ntm * ntn;
-  const char* pe = getenv("MIFT_LM_PERSIST");  // read per call: A/B-able within one process
-  const bool persist = (pe ? atoi(pe) != 0 : true) && K / BK >= 2;
+  // persistent kernel at K <= 1024 (12 k-tiles per tile at distilgpt2's K = 768: the per-tile prologue
+  // and epilogue are a large share; 664 vs 723 us), the one-tile kernel above (OPT K = 2560: 40 k-tiles
+  // per tile, 1350 vs 1394 us with the raster group of both) — profiles/r5/bench_lm_persist_v2.jsonl.
+  // MIFT_LM_PERSIST=0/1 forces either (read per call: A/B-able).  Even M: the ids copy moves 16-B pairs.
+  const char* pe = getenv("MIFT_LM_PERSIST");
+  const bool persist = (pe ? atoi(pe) != 0 : K <= 1024) && K / BK >= 2 && M >= 2 && M % 2 == 0;
   if (persist) {
     const int G = std::min(grid, num_cus());  // one 512-thread, 137 KiB block per CU
     hipLaunchKernelGGL(kernp, dim3(G), dim3(512), SMEM_P, st, (const T*)a.data_ptr(), (const T*)w.data_ptr(),
