@@ -247,8 +247,12 @@ def main():
     trace = os.environ.get("MIFT_BENCH_TRACE") == "1"  # diagnostics: per-step host ms to stderr
     sync_every = int(os.environ.get("MIFT_BENCH_SYNC", "0"))  # diagnostics: host sync every k steps
     t0 = time.perf_counter()
+    last = t0
     for i in range(a.warmup, total_steps):
         run(i)
+        if not trace and ctx.rank == 0 and time.perf_counter() - last > 30.0:
+            last = time.perf_counter()
+            print(f"bench.py: step {i + 1 - a.warmup}/{a.steps} {last - t0:.1f}s", file=sys.stderr, flush=True)
         if trace or (sync_every and (i + 1) % sync_every == 0):
             sync()
         if trace:
@@ -291,8 +295,13 @@ def main():
             if dist.is_initialized():
                 dist.barrier()
             te = time.perf_counter()
-            for s_ in eb_steps:
+            last = te
+            for k, s_ in enumerate(eb_steps):
                 trainer.train_step(s_)
+                now = time.perf_counter()
+                if now - last > 30.0 and ctx.rank == 0:  # progress (a silent multi-minute run looks hung)
+                    print(f"bench.py: epoch step {k + 1}/{len(eb_steps)} {now - te:.1f}s", file=sys.stderr, flush=True)
+                    last = now
             sync()
             if dist.is_initialized():
                 dist.barrier()
