@@ -306,7 +306,7 @@ def test_flash_attention_kv_len():
 
 
 @pytest.mark.parametrize("p", [0.0, 0.05])
-@pytest.mark.parametrize("K", [768, 2304, 3072, 2560])
+@pytest.mark.parametrize("K", [768, 2304, 3072, 2560, 4096])
 @pytest.mark.parametrize("M,nz", [(1000, 8), (1000, 24), (24576, 8)])
 def test_lora_proj_and_wgrad(p, K, M, nz):
     """lora_proj for every block geometry (16- and 32-row blocks, one or two 16-column tiles:
@@ -454,13 +454,14 @@ def test_grad_stats_deterministic():
     assert stats[1].item() == 2.0
 
 
-@pytest.mark.parametrize("rank,D", [(8, 768), (28, 768), (28, 2560), (16, 1024)])
+@pytest.mark.parametrize("rank,D", [(8, 768), (28, 768), (28, 2560), (8, 2560), (16, 1024), (8, 2048), (28, 4096),
+                                    (8, 1536)])
 @pytest.mark.parametrize("p", [0.0, 0.05])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_rowproj_fused_kernels(rank, D, p, dt):
     """LN fwd + LoRA projection and dropout-bwd + dT (csrc/kernels/rowproj.hip) vs fp32 reference.
-    D in {768, 1024} runs the MFMA 16-row form (rank 28: two 16-column output tiles), 2560 the
-    one-wave-per-row form; M = 777 leaves a partial last 16-row tile."""
+    D in {768, 1024, 2048, 2560, 4096} runs the MFMA 16-row form on 4 / 8 / 16 waves (rank 28: two
+    16-column output tiles), 1536 the one-wave-per-row form; M = 777 leaves a partial last 16-row tile."""
     C = _C()
     torch.manual_seed(11)
     M = 777
@@ -671,14 +672,21 @@ def test_gemm_ln_prologue(M, N, K, act):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,rank,p,dres,wf32", [(768, 8, 0.1, True, False), (768, 24, 0.0, True, False),
-                                               (1024, 8, 0.1, False, True), (768, 8, 0.1, True, True)])
-def test_ln_bwd_mask_proj_matches_separate_passes(D, rank, p, dres, wf32):
+@pytest.mark.parametrize("D,rank,p,dres,wf32,dt", [(768, 8, 0.1, True, False, torch.bfloat16),
+                                                  (768, 24, 0.0, True, False, torch.bfloat16),
+                                                  (1024, 8, 0.1, False, True, torch.bfloat16),
+                                                  (768, 8, 0.1, True, True, torch.bfloat16),
+                                                  (2560, 24, 0.1, True, False, torch.float16),
+                                                  (2560, 8, 0.0, False, True, torch.float16),
+                                                  (2048, 8, 0.1, True, False, torch.bfloat16),
+                                                  (2560, 8, 0.1, True, True, torch.bfloat16)])
+def test_ln_bwd_mask_proj_matches_separate_passes(D, rank, p, dres, wf32, dt):
     """rowproj MODE 3 (LN backward + residual-dropout backward + dT projection in one pass) against
-    layer_norm_bwd followed by mask_proj, and against the fp32 reference of the three ops."""
+    layer_norm_bwd followed by mask_proj, and against the fp32 reference of the three ops (the OPT
+    widths run the 8- and 16-wave forms)."""
     from mift.ops import kernels as K
     torch.manual_seed(3)
-    M, dt = 1000, torch.bfloat16
+    M = 1000
     x = torch.randn(M, D, device="cuda").to(dt)
     dy = torch.randn(M, D, device="cuda").to(dt)
     w = (1 + 0.1 * torch.randn(D, device="cuda")).to(torch.float32 if wf32 else dt)

@@ -1,4 +1,5 @@
-"""Same-process A/B of whole training steps (distilgpt2 bench config, hipGraph replay).
+"""Same-process A/B of whole training steps (distilgpt2 bench config, or OPT at micro-batch 12 x 512
+fp16 with --model opt-2.7b; hipGraph replay).
 
 Whole-process bench.py runs on one box differ by up to ~10 % from process to process, which
 hides few-percent kernel changes.  Here two (or more) trainers are built in ONE process, each
@@ -31,6 +32,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--model", default="distilgpt2")
+    ap.add_argument("--mb", type=int, default=None, help="rows per step (default 32; OPT: 12 x 512 tokens)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     import torch
@@ -41,25 +43,28 @@ def main():
     from mift.train.trainer import TrainConfig, Trainer
 
     ctx = D.init(verbose=False)
-    per_rank, seq = 32, 256
+    opt = "opt" in a.model
+    per_rank, seq = (a.mb or 12, 512) if opt else (a.mb or 32, 256)
+    prec = "fp16" if opt else "bf16"
+    targets = ["q_proj", "k_proj", "v_proj", "out_proj", "fc1", "fc2"] if opt else ["c_attn", "c_proj"]
     trainers = []
     for spec in a.configs:
         env = parse_env(spec)
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        model = build_causal_lm(a.model, dtype=torch.bfloat16, device=ctx.device, seed=0)
+        model = build_causal_lm(a.model, dtype=torch.float16 if opt else torch.bfloat16, device=ctx.device, seed=0)
         # diagnostics only: AB_LORA_P / AB_MODEL_PDROP change the dropout rates of this arm
         lp = float(env.get("AB_LORA_P", 0.05))
         if "AB_MODEL_PDROP" in env:
             for k in ("attn_pdrop", "resid_pdrop", "embd_pdrop"):
                 setattr(model.config, k, float(env["AB_MODEL_PDROP"]))
-        L.inject(model, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=lp, target_modules=["c_attn", "c_proj"],
+        L.inject(model, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=lp, target_modules=targets,
                                      base_model_name_or_path=a.model))
         n = per_rank * (a.blocks * a.steps + 4)
         ds = synthetic_openwebtext(n, seq, model.config.vocab_size, model.config.pad_token_id, seed=1234,
                                    full_length=True)
         b = MicroBatcher(ds, per_rank, 1, rank=0, world=1)
-        tr = Trainer(model, b, TrainConfig(epochs=1, batch=per_rank, accum=1, lr=5e-5, precision="bf16",
+        tr = Trainer(model, b, TrainConfig(epochs=1, batch=per_rank, accum=1, lr=5e-5, precision=prec,
                                            logging_steps=0, save_steps=0, step_log="none"), ctx)
         model.train()
         steps = list(b.epoch(0))

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void mask_proj_kernel(const T* __restrict__ x,
   reduce_store<T, LR>(acc, pout + (size_t)row * 32, lane, alpha);
 }
 
-// ---- MFMA form (D = 32·NK, NK in {24, 32}): one 4-wave block per 16 rows ----
+// ---- MFMA form (D = 32·NK): one NW-wave block per 16 rows (NW = 4 / 8 / 16 by width, by_nk) ----
 // The one-wave-per-row kernels above re-read the [LR, D] projection operand from cache for every
 // row and do LR dot2 per element pair on the VALU: at LR = 32 (OPT's three q/k/v adapters) they
 // ran 136 us at M = 16384, D = 768, 10x the LN alone.  Here a block owns a 16-row MFMA A-tile and
@@ -242,8 +242,8 @@ __global__ __launch_bounds__(256) void mask_proj_kernel(const T* __restrict__ x,
 // weight, mean_out / rstd_out its saved statistics (read); dh = LN-bwd(dY) + dres is stored (the
 // residual-stream gradient), then MODE 0 on the rounded dh (the upstream LoRA linear's dropout and
 // dT = s·y·Bᵀ) — the separate MODE 0 pass re-read dh (one launch and 12.6 MB per site at distilgpt2).
-template <typename T, typename W, int NK, int NTI, int MODE>
-__global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__ x, const W* __restrict__ lw,
+template <typename T, typename W, int NK, int NTI, int MODE, int NW>
+__global__ __launch_bounds__(NW * 64) void rowproj_mfma_kernel(const T* __restrict__ x, const W* __restrict__ lw,
                                                            const W* __restrict__ lb, T* __restrict__ y,
                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                            const T* __restrict__ pw, T* __restrict__ pout, int M,
@@ -254,10 +254,10 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
                                                            T* __restrict__ dh) {
   using frag = typename std::conditional<std::is_same<T, bf16>::value, bf16x8, fp16x8>::type;
   constexpr int D = NK * 32;
-  constexpr int NKW = NK / 4;  // k-steps per wave
-  static_assert(NK % 4 == 0, "k-steps split over 4 waves");
-  __shared__ float red[4][16];
-  __shared__ float pred[4][16][33];
+  constexpr int NKW = NK / NW;  // k-steps per wave
+  static_assert(NK % NW == 0, "k-steps split evenly over the waves");
+  __shared__ float red[NW][16];
+  __shared__ float pred[NW][16][33];
   seed = mift_seed(seed, sstep);
   const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -270,13 +270,15 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
 #pragma unroll
   for (int s = 0; s < NKW; ++s) xv[s] = *reinterpret_cast<const short8*>(xr + s * 32);
   T* yr = y + (size_t)row * D + c00;
-  // sum over the block's 4 waves of a per-row value held by lanes g = 0..3 of every wave
+  // sum over the block's NW waves (in wave order) of a per-row value held by lanes g = 0..3 of every wave
   auto row_sum = [&](float v) {
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
     if (g == 0) red[wave][fr] = v;
     __syncthreads();
-    const float r = red[0][fr] + red[1][fr] + red[2][fr] + red[3][fr];
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) r += red[q][fr];
     __syncthreads();  // red is reused by the next call
     return r;
   };
@@ -321,30 +323,48 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
     }
   } else if constexpr (MODE == 3) {
     const float mean = mean_out[row], rstd = rstd_out[row];
-    short8 hv[NKW], rv[NKW];
+    // the 4-wave widths (768 / 1024) request dres with the other row operands; the wide forms (8 / 16
+    // waves, up to 10 pieces per operand) load it in the output loop: all three operands live across
+    // the statistics barrier spilled 114-253 VGPRs there
+    constexpr bool RV_EARLY = NW == 4;
+    short8 hv[NKW], rv[RV_EARLY ? NKW : 1];
     const T* hr = xin + (size_t)row * D + c00;
 #pragma unroll
     for (int s = 0; s < NKW; ++s) {
       hv[s] = *reinterpret_cast<const short8*>(hr + s * 32);
-      rv[s] = dres != nullptr ? *reinterpret_cast<const short8*>(dres + (size_t)row * D + c00 + s * 32)
-                              : short8{0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (RV_EARLY)
+        rv[s] = dres != nullptr ? *reinterpret_cast<const short8*>(dres + (size_t)row * D + c00 + s * 32)
+                                : short8{0, 0, 0, 0, 0, 0, 0, 0};
     }
     float sg = 0.f, sgx = 0.f;
+    // wide forms: the per-step LN weight / dres loads go one step ahead of their use, and a scheduling
+    // barrier per step keeps hipcc from hoisting every step's loads to the top of the unrolled loop
+    // (what made the register footprint)
+    float wn[8];
+    short8 rn = short8{0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (!RV_EARLY) load8<W>(lw + c00, wn);
 #pragma unroll
     for (int s = 0; s < NKW; ++s) {
       float dv[8], xf[8], wv[8];
       unpack8<T>(xv[s], dv);
       unpack8<T>(hv[s], xf);
-      load8<W>(lw + c00 + s * 32, wv);
+      if constexpr (RV_EARLY) {
+        load8<W>(lw + c00 + s * 32, wv);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wv[e] = wn[e];
+        load8<W>(lw + c00 + min(s + 1, NKW - 1) * 32, wn);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float gg = dv[e] * wv[e];
         sg += gg;
         sgx += gg * ((xf[e] - mean) * rstd);
       }
+      if constexpr (!RV_EARLY) __builtin_amdgcn_sched_barrier(0);
     }
     {  // both row sums in one LDS exchange (one barrier pair instead of two)
-      __shared__ float red2[4][16][2];
+      __shared__ float red2[NW][16][2];
       sg += __shfl_xor(sg, 16, 64);
       sg += __shfl_xor(sg, 32, 64);
       sgx += __shfl_xor(sgx, 16, 64);
@@ -353,9 +373,19 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
         red2[wave][fr][0] = sg;
         red2[wave][fr][1] = sgx;
       }
+      if constexpr (!RV_EARLY) {  // step 0's operands requested before the barrier
+        load8<W>(lw + c00, wn);
+        if (dres != nullptr) rn = *reinterpret_cast<const short8*>(dres + (size_t)row * D + c00);
+      }
       __syncthreads();
-      sg = (red2[0][fr][0] + red2[1][fr][0] + red2[2][fr][0] + red2[3][fr][0]) * (1.f / D);
-      sgx = (red2[0][fr][1] + red2[1][fr][1] + red2[2][fr][1] + red2[3][fr][1]) * (1.f / D);
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        s0 += red2[q][fr][0];
+        s1 += red2[q][fr][1];
+      }
+      sg = s0 * (1.f / D);
+      sgx = s1 * (1.f / D);
     }
     T* dhr = dh + (size_t)row * D + c00;
 #pragma unroll
@@ -363,8 +393,17 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
       float dv[8], xf[8], wv[8], r[8], o[8];
       unpack8<T>(xv[s], dv);
       unpack8<T>(hv[s], xf);
-      unpack8<T>(rv[s], r);
-      load8<W>(lw + c00 + s * 32, wv);
+      if constexpr (RV_EARLY) {
+        unpack8<T>(rv[s], r);
+        load8<W>(lw + c00 + s * 32, wv);
+      } else {
+        unpack8<T>(rn, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wv[e] = wn[e];
+        const int sn = min(s + 1, NKW - 1);
+        load8<W>(lw + c00 + sn * 32, wn);
+        if (dres != nullptr) rn = *reinterpret_cast<const short8*>(dres + (size_t)row * D + c00 + sn * 32);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = rstd * (dv[e] * wv[e] - sg - (xf[e] - mean) * rstd * sgx) + r[e];
       short8 hq;
@@ -386,6 +425,7 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
         if (live) *reinterpret_cast<short8*>(yr + s * 32) = hq;
       }
       xv[s] = hq;
+      if constexpr (!RV_EARLY) __builtin_amdgcn_sched_barrier(0);
     }
   } else if (MODE == 0 && thr != 0) {  // residual-dropout backward: y = keep ? x/(1-p) : 0, stored and projected
 #pragma unroll
@@ -441,38 +481,50 @@ __global__ __launch_bounds__(256) void rowproj_mfma_kernel(const T* __restrict__
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bfv, acc[j], 0, 0, 0);
     }
   }
-  // lane (fr, g) holds the partial out[4g + r][16j + fr]; sum the 4 waves' partials in LDS
+  // lane (fr, g) holds the partial out[4g + r][16j + fr]; sum the NW waves' partials in LDS (wave order)
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int j = 0; j < 2; ++j) pred[wave][4 * g + r][j * 16 + fr] = j < NTI ? acc[j < NTI ? j : 0][r] : 0.f;
   __syncthreads();
-  for (int e = tid; e < 16 * 32; e += 256) {
+  for (int e = tid; e < 16 * 32; e += NW * 64) {
     const int r = e >> 5, c = e & 31;
-    if (m0 + r < M)
-      pout[(size_t)(m0 + r) * 32 + c] = (T)((pred[0][r][c] + pred[1][r][c] + pred[2][r][c] + pred[3][r][c]) * alpha);
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) v += pred[q][r][c];
+    if (m0 + r < M) pout[(size_t)(m0 + r) * 32 + c] = (T)(v * alpha);
   }
 }
 
-// D = 32·NK with NK in {24, 32} (distilgpt2 / OPT-125m 768, 1024); false: use the row kernels
+// MFMA-form widths: D = 32·NK, split over NW waves (NK / NW k-steps of 32 columns per wave, so a wave
+// holds <= 10 16-B pieces of each row operand): 768 / 1024 on 4 waves (distilgpt2, OPT-125m / 350m),
+// 2048 / 2560 on 8 (OPT-1.3b / 2.7b), 4096 on 16 (OPT-6.7b).  MIFT_ROWPROJ_V=1 (A/B knob, read per
+// call): the row kernels.  Other widths take the row kernels (the LN / mask producers) or lora_proj.
+inline bool rowproj_width(int D) { return D == 768 || D == 1024 || D == 2048 || D == 2560 || D == 4096; }
 inline bool rowproj_mfma_ok(int D) {
-  const char* e = getenv("MIFT_ROWPROJ_V");  // 1 = the row kernels (A/B knob, read per call)
-  return !(e && atoi(e) == 1) && (D == 768 || D == 1024);
+  const char* e = getenv("MIFT_ROWPROJ_V");
+  return !(e && atoi(e) == 1) && rowproj_width(D);
 }
 
+// f(integral_constant NK, integral_constant NW) for a rowproj_width D
 template <typename F>
 void by_nk(int D, F&& f) {
-  if (D == 768) f(std::integral_constant<int, 24>{});
-  else f(std::integral_constant<int, 32>{});
+  using std::integral_constant;
+  switch (D) {
+    case 768: f(integral_constant<int, 24>{}, integral_constant<int, 4>{}); break;
+    case 1024: f(integral_constant<int, 32>{}, integral_constant<int, 4>{}); break;
+    case 2048: f(integral_constant<int, 64>{}, integral_constant<int, 8>{}); break;
+    case 2560: f(integral_constant<int, 80>{}, integral_constant<int, 8>{}); break;
+    default: f(integral_constant<int, 128>{}, integral_constant<int, 16>{}); break;  // 4096
+  }
 }
 
+// the plain projection (MODE 2): the rowproj widths plus K = 2304 (distilgpt2's c_attn dT)
+inline bool rowproj_proj_width(int K) { return rowproj_width(K) || K == 2304; }
 template <typename F>
-void by_nk_proj(int D, F&& f) {
-  switch (D) {
-    case 768: f(std::integral_constant<int, 24>{}); break;
-    case 1024: f(std::integral_constant<int, 32>{}); break;
-    default: f(std::integral_constant<int, 72>{}); break;  // 2304
-  }
+void by_nk_proj(int K, F&& f) {
+  if (K == 2304) f(std::integral_constant<int, 72>{}, std::integral_constant<int, 4>{});
+  else by_nk(K, f);
 }
 
 template <int LR, typename F>
@@ -529,10 +581,10 @@ std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::
     auto go2 = [&](auto tt, auto wt) {
       using T = decltype(tt);
       using Wt = decltype(wt);
-      by_nk(D, [&](auto nk) {
-        constexpr int NK = decltype(nk)::value;
-        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, Wt, NK, 1, 1> : rowproj_mfma_kernel<T, Wt, NK, 2, 1>;
-        hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(),
+      by_nk(D, [&](auto nk, auto nw) {
+        constexpr int NK = decltype(nk)::value, NW = decltype(nw)::value;
+        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, Wt, NK, 1, 1, NW> : rowproj_mfma_kernel<T, Wt, NK, 2, 1, NW>;
+        hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(NW * 64), 0, st, (const T*)x.data_ptr(),
                            (const Wt*)w.data_ptr(), (const Wt*)b.data_ptr(), (T*)y.data_ptr(), mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, (float)eps,
                            (float)alpha * inv, (uint64_t)seed, mift_seed_step(), thr, inv, (int)rank, 1,
@@ -588,10 +640,10 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
   if (rowproj_mfma_ok(D)) {
     auto go2 = [&](auto tt) {
       using T = decltype(tt);
-      by_nk(D, [&](auto nk) {
-        constexpr int NK = decltype(nk)::value;
-        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, T, NK, 1, 0> : rowproj_mfma_kernel<T, T, NK, 2, 0>;
-        hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
+      by_nk(D, [&](auto nk, auto nw) {
+        constexpr int NK = decltype(nk)::value, NW = decltype(nw)::value;
+        auto kern = rank <= 16 ? rowproj_mfma_kernel<T, T, NK, 1, 0, NW> : rowproj_mfma_kernel<T, T, NK, 2, 0, NW>;
+        hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(NW * 64), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
                            (const T*)nullptr, (T*)y.data_ptr(), (float*)nullptr, (float*)nullptr,
                            (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M, 0.f, (float)alpha, (uint64_t)seed,
                            mift_seed_step(), thr, inv, (int)rank, thr != 0 ? 1 : 0, (const T*)nullptr,
@@ -621,8 +673,10 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
 
 // (dh, y, proj[M,32]): dh = LN-bwd(dy; x, w, mean, rstd) + dres, y = keep⊙dh/(1-p) (dh itself when
 // p == 0), proj = alpha·y·pw^T — layer_norm_bwd followed by mask_proj in one pass (MFMA form only:
-// D in {768, 1024}; the caller checks mift_ln_bwd_mask_proj_ok)
-bool mift_ln_bwd_mask_proj_ok(int64_t D) { return rowproj_mfma_ok((int)D); }
+// the rowproj widths; the caller checks mift_ln_bwd_mask_proj_ok)
+// (not at 4096: the 16-wave MODE 3 form spills ~110 VGPRs at its 128-register budget and ran 155 us
+// against 81 for layer_norm_bwd + mask_scale + lora_proj at M = 6144, tools/bench_rowproj_opt.py)
+bool mift_ln_bwd_mask_proj_ok(int64_t D) { return rowproj_mfma_ok((int)D) && D != 4096; }
 
 std::vector<at::Tensor> mift_ln_bwd_mask_proj(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
                                               const at::Tensor& mean, const at::Tensor& rstd,
@@ -632,7 +686,7 @@ std::vector<at::Tensor> mift_ln_bwd_mask_proj(const at::Tensor& dy, const at::Te
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf, "ln_bwd_mask_proj: bf16/fp16");
   const int D = dy.size(1);
   const int M = dy.size(0);
-  TORCH_CHECK(rowproj_mfma_ok(D), "ln_bwd_mask_proj: D in {768, 1024}");
+  TORCH_CHECK(mift_ln_bwd_mask_proj_ok(D), "ln_bwd_mask_proj: D in {768, 1024, 2048, 2560}");
   TORCH_CHECK(x.is_contiguous() && x.sizes() == dy.sizes() && x.scalar_type() == dy.scalar_type(), "ln_bwd_mask_proj: x");
   TORCH_CHECK(!dres || (dres->is_contiguous() && dres->sizes() == dy.sizes() && dres->scalar_type() == dy.scalar_type()),
               "ln_bwd_mask_proj: dres");
@@ -651,10 +705,10 @@ std::vector<at::Tensor> mift_ln_bwd_mask_proj(const at::Tensor& dy, const at::Te
   auto go = [&](auto tt, auto wt) {
     using T = decltype(tt);
     using Wt = decltype(wt);
-    by_nk(D, [&](auto nk) {
-      constexpr int NK = decltype(nk)::value;
-      auto kern = rank <= 16 ? rowproj_mfma_kernel<T, Wt, NK, 1, 3> : rowproj_mfma_kernel<T, Wt, NK, 2, 3>;
-      hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)dy.data_ptr(), (const Wt*)w.data_ptr(),
+    by_nk(D, [&](auto nk, auto nw) {
+      constexpr int NK = decltype(nk)::value, NW = decltype(nw)::value;
+      auto kern = rank <= 16 ? rowproj_mfma_kernel<T, Wt, NK, 1, 3, NW> : rowproj_mfma_kernel<T, Wt, NK, 2, 3, NW>;
+      hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(NW * 64), 0, st, (const T*)dy.data_ptr(), (const Wt*)w.data_ptr(),
                          (const Wt*)nullptr, (T*)y.data_ptr(), const_cast<float*>(mean.data_ptr<float>()),
                          const_cast<float*>(rstd.data_ptr<float>()), (const T*)pw.data_ptr(), (T*)pout.data_ptr(), M,
                          0.f, (float)alpha, (uint64_t)seed, mift_seed_step(), thr, inv, (int)rank, thr != 0 ? 1 : 0,
@@ -670,7 +724,7 @@ std::vector<at::Tensor> mift_ln_bwd_mask_proj(const at::Tensor& dy, const at::Te
   return {dh, y, pout};
 }
 
-// lora_proj on the 4-wave 16-row MFMA form (MODE 2) for contiguous x at K in {768, 1024, 2304}:
+// lora_proj on the 16-row MFMA form (MODE 2) for contiguous x at the rowproj widths and K = 2304:
 // out = alpha·(1/(1-p))·drop(x)·wᵀ.  Returns false (caller runs lora_proj's own kernel) otherwise.
 // lora_proj's own kernel (16-row blocks, K split over the waves, 8 k-steps of loads in flight) ran
 // 8.5 / 20.2 us at M = 8192, K = 768 / 2304 against 6.4 / 18.2 here (profiles/r3/bench_rowproj_r3k.jsonl).
@@ -679,7 +733,7 @@ bool mift_rowproj_lora_proj(const at::Tensor& x, const at::Tensor& w, at::Tensor
   const int M = x.size(0), K = x.size(1);
   const char* e = getenv("MIFT_ROWPROJ_V");  // 1 = off (A/B knob, read per call)
   // (K = 3072 measured slower here than lora_proj's kernel: 24.2 vs 21.9 us at M = 8192)
-  if ((e && atoi(e) == 1) || !(K == 768 || K == 1024 || K == 2304) || x.stride(0) != K ||
+  if ((e && atoi(e) == 1) || !rowproj_proj_width(K) || x.stride(0) != K ||
       reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 != 0)
     return false;
   if (M == 0) return true;
@@ -688,10 +742,10 @@ bool mift_rowproj_lora_proj(const at::Tensor& x, const at::Tensor& w, at::Tensor
   const float ik = p > 0 ? mift_inv_keep(p) : 1.f;
   auto go = [&](auto tt) {
     using T = decltype(tt);
-    by_nk_proj(K, [&](auto nk) {
-      constexpr int NK = decltype(nk)::value;
-      auto kern = rows <= 16 ? rowproj_mfma_kernel<T, T, NK, 1, 2> : rowproj_mfma_kernel<T, T, NK, 2, 2>;
-      hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(256), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
+    by_nk_proj(K, [&](auto nk, auto nw) {
+      constexpr int NK = decltype(nk)::value, NW = decltype(nw)::value;
+      auto kern = rows <= 16 ? rowproj_mfma_kernel<T, T, NK, 1, 2, NW> : rowproj_mfma_kernel<T, T, NK, 2, 2, NW>;
+      hipLaunchKernelGGL(kern, dim3((M + 15) / 16), dim3(NW * 64), 0, st, (const T*)x.data_ptr(), (const T*)nullptr,
                          (const T*)nullptr, (T*)nullptr, (float*)nullptr, (float*)nullptr, (const T*)w.data_ptr(),
                          (T*)out.data_ptr(), M, 0.f, (float)alpha * ik, (uint64_t)seed, mift_seed_step(), thr, ik,
                          (int)rows, 0, (const T*)nullptr, (const T*)nullptr, (T*)nullptr);

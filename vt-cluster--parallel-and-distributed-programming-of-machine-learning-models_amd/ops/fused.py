@@ -30,12 +30,17 @@ import torch
 from . import kernels as K
 from .streams import join as join_side, run_side
 
-# LN fused with the LoRA input projection does LR FMAs per element on the VALU with the [LR,D]
-# operand re-read from cache for every row: a win for one adapter (LR = 8), but for OPT's fused
-# q/k/v adapters (24 rows -> LR = 32) it ran 475 us at M = 24576, D = 2560 against LN + the MFMA
-# lora_proj (tools/bench_rowproj.py) — above this many rows, LN and projection run separately.
-# One adapter at OPT's D = 2560 lost too (125 us vs 46 + 40 us); at distilgpt2's D = 768 it is even
-# (17.2 vs 7.6 + 8.9 us) and saves a launch.
+# The fused row passes (LN / dropout-bwd / LN-bwd + the LoRA projection, csrc/kernels/rowproj.hip) run
+# their MFMA 16-row form at the widths below (4 waves per block at 768 / 1024, 8 at 2048 / 2560, 16 at
+# 4096: OPT-125m .. 6.7b), per pass where it measured no slower than the separate passes it replaces
+# (tools/bench_rowproj_opt.py at M = 6144, fp16; profiles/r5/bench_rowproj_opt.json): the LN forward +
+# projection not at 4096 (42.4 vs 40.8 us), the LN backward + dropout backward + dT not at 4096 (the
+# 16-wave form spills: 155 vs 81 us).  Elsewhere only the one-wave-per-row kernels exist, which do LR
+# FMAs per element on the VALU with the [LR,D] operand re-read from cache for every row: for OPT's fused
+# q/k/v adapters (24 rows -> LR = 32) at D = 2560 they ran 131 us at M = 6144 against 27 for LN + the
+# MFMA lora_proj, so there they are limited to few rows and D <= 1024.
+_ROWPROJ_D = {"ln": (768, 1024, 2048, 2560), "mask": (768, 1024, 2048, 2560, 4096),
+              "ln_bwd": (768, 1024, 2048, 2560)}
 
 
 def _diag_skip(what):
@@ -47,24 +52,30 @@ _LNPROJ_MAX_ROWS = int(os.environ.get("MIFT_LNPROJ_MAX_ROWS", "8"))
 _LNPROJ_MAX_D = int(os.environ.get("MIFT_LNPROJ_MAX_D", "1024"))
 
 
-def _rowproj_fused(D, rows):
-    """One fused row pass (LN / dropout-bwd + projection): the MFMA 16-row kernel at D in {768, 1024}
+def _mfma_width(D, kind):
+    """The MFMA row-pass form runs pass ``kind`` ("ln", "mask", "ln_bwd") at width D
+    (MIFT_ROWPROJ_WIDE=0, read per call: only the round-4 widths 768 / 1024 — A/B knob)."""
+    return D in (768, 1024) or (D in _ROWPROJ_D[kind] and os.environ.get("MIFT_ROWPROJ_WIDE", "1") != "0")
+
+
+def _rowproj_fused(D, rows, kind):
+    """One fused row pass (LN / dropout-bwd + projection): the MFMA 16-row kernel where _mfma_width
     (any rank), the one-wave-per-row kernel for up to _LNPROJ_MAX_ROWS rows at other D <= 1024."""
-    return D in (768, 1024) or (rows <= _LNPROJ_MAX_ROWS and D <= _LNPROJ_MAX_D)
+    return _mfma_width(D, kind) or (rows <= _LNPROJ_MAX_ROWS and D <= _LNPROJ_MAX_D)
 
 
 def _ln_fwd_lora(x2, ln_w, ln_b, eps, lo, seed, training):
     """(LN(x), mean, rstd, T32 = s·dropout(LN(x))·Aᵀ) — fused row pass or LN + lora_proj."""
-    if _rowproj_fused(x2.shape[-1], lo.rows):
+    if _rowproj_fused(x2.shape[-1], lo.rows, "ln"):
         return K.layer_norm_fwd_proj(x2, ln_w, ln_b, eps, lo.A32s, lo.rows, 1.0, lo.p if training else 0.0, seed)
     a, mean, rstd = K.layer_norm_fwd(x2, ln_w, ln_b, eps)
     return a, mean, rstd, lo.forward(a, seed, training)
 
 
 def _mask_proj(g2, p, seed, lo):
-    """(gz = dropout-bwd(g), dT0 = dt_alpha·gz·B) — one row pass at small D; at OPT's D = 2560 the
-    row pass (79 us) lost to mask_scale + the hipBLASLt projection (38 + 22 us)."""
-    if _rowproj_fused(g2.shape[-1], lo.rows):
+    """(gz = dropout-bwd(g), dT0 = dt_alpha·gz·B) — one row pass where _rowproj_fused (the one-wave-per-row
+    form at OPT's D = 2560 ran 79 us against mask_scale + the projection, 38 + 22 us)."""
+    if _rowproj_fused(g2.shape[-1], lo.rows, "mask"):
         return K.mask_proj(g2, p, seed, lo.B32t, lo.rows, lo.dt_alpha)
     gz = K.mask_scale(g2, p, seed) if p > 0 else g2
     return gz, K.lora_proj(gz, lo.B32t, lo.dt_alpha, 0.0, 0, rows=lo.rows)
@@ -362,7 +373,7 @@ class GradHandoff:
 
     def ready(self, D):
         return (self.lo is not None and os.environ.get("MIFT_LN_MASK_PROJ", "1") != "0"
-                and K.ln_bwd_mask_proj_ok(D))
+                and _mfma_width(D, "ln_bwd") and K.ln_bwd_mask_proj_ok(D))
 
     def ln_bwd(self, da, x2, ln_w, mean, rstd, dres):
         """LN backward (+ dres); with a registered consumer also its mask_proj, kept for it."""
