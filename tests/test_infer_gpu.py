@@ -136,8 +136,9 @@ def test_decode_attn_device_position_matches_host():
 
 @pytest.mark.parametrize("name", ["gpt2", "opt"])
 def test_graphed_decode_matches_eager(name, monkeypatch):
-    """Decode steps replayed from one hipGraph (device-side position / flags / output column) give the
-    eager loop's tokens exactly, for left-padded batches and with HF's stop-when-all-finished rule."""
+    """A whole generate() call replayed from one hipGraph (prefill + device-side position / flags / output
+    column) gives the eager loop's tokens exactly, for left-padded batches, for new inputs of a cached
+    shape and with HF's stop-when-all-finished rule."""
     from mift.apps.gen_probe import distinct_prompts
     from mift.infer import generate as G
     from mift.models.gpt2 import GPT2Config, GPT2LMHeadModel
@@ -162,6 +163,14 @@ def test_graphed_decode_matches_eager(name, monkeypatch):
 
     e, g1, g2 = both(max_new_tokens=12, eos_token_id=-1)
     assert e.shape == (16, ids.shape[1] + 12) and torch.equal(e, g1) and torch.equal(e, g2)
+    # the cached whole-call graph (prefill included) on NEW inputs of the same shape: rows reordered,
+    # so every row's prompt length and tokens change
+    ids_f, mask_f = ids.flip(0).contiguous(), mask.flip(0).contiguous()
+    monkeypatch.setenv("MIFT_GEN_GRAPH", "0")
+    e_f = G.generate(m, ids_f, attention_mask=mask_f, max_new_tokens=12, eos_token_id=-1)
+    monkeypatch.setenv("MIFT_GEN_GRAPH", "1")
+    g_f = G.generate(m, ids_f, attention_mask=mask_f, max_new_tokens=12, eos_token_id=-1)
+    assert torch.equal(e_f, g_f) and torch.equal(e_f, e.flip(0))
     # early stop: identical prompts -> identical rows; EOS := the 4th generated token
     same = ids[:1].expand(4, -1).contiguous()
     msk = mask[:1].expand(4, -1).contiguous()

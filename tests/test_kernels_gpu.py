@@ -671,6 +671,46 @@ def test_gemm_ln_prologue(M, N, K, act):
     torch.testing.assert_close(y.float(), ref_y, atol=6e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("M", [1, 13, 64])
+@pytest.mark.parametrize("N,K,act,dt", [(2304, 768, 0, torch.bfloat16), (3072, 768, 1, torch.bfloat16),
+                                        (1024, 1024, 2, torch.float16), (768, 768, 0, torch.float16)])
+def test_gemm_ln_fold(M, N, K, act, dt):
+    """gemm_ln_fold (decode, LN folded into the weights: rstd·(x·(γ∘w)ᵀ − mean·c1) + c2) against the fp32
+    reference of act(LayerNorm(x) @ w.T + bias), at GPT-2-like residual rows (mean offset, one outlier
+    column), and against the LN-prologue form; the fold cache is rebuilt after an in-place update."""
+    from mift.ops import fused as F
+    from mift.ops import kernels as K_
+    torch.manual_seed(5)
+    x = torch.randn(M, K, device="cuda") * 3 + 1
+    x[:, 7] = 40.0  # an outlier dimension as in GPT-2's residual stream
+    x = x.to(dt)
+    ln = torch.nn.LayerNorm(K, eps=1e-5, device="cuda", dtype=dt)
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.1 * torch.randn(K, device="cuda"))
+        ln.bias.copy_(0.1 * torch.randn(K, device="cuda"))
+
+    class Lin:
+        pass
+
+    lin = Lin()
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(dt)
+    lin.bias = (0.1 * torch.randn(N, device="cuda")).to(dt)
+    y = F._gemm_ln(x, ln, lin, w, act=act)
+    ref_a = torch.nn.functional.layer_norm(x.float(), (K,), ln.weight.float(), ln.bias.float(), 1e-5)
+    z = ref_a @ w.float().t() + lin.bias.float()
+    ref_y = {0: z, 1: torch.nn.functional.gelu(z, approximate="tanh"), 2: torch.relu(z)}[act]
+    torch.testing.assert_close(y.float(), ref_y, atol=6e-2, rtol=3e-2)
+    y1 = K_.gemm_ln(x, ln.weight, ln.bias, 1e-5, w, lin.bias, act=act)
+    torch.testing.assert_close(y.float(), y1.float(), atol=8e-2, rtol=3e-2)
+    with torch.no_grad():
+        ln.weight.mul_(2.0)  # in place: version counter bumps, the folded operands must follow
+    y2 = F._gemm_ln(x, ln, lin, w, act=act)
+    ref_a2 = torch.nn.functional.layer_norm(x.float(), (K,), ln.weight.float(), ln.bias.float(), 1e-5)
+    z2 = ref_a2 @ w.float().t() + lin.bias.float()
+    ref_y2 = {0: z2, 1: torch.nn.functional.gelu(z2, approximate="tanh"), 2: torch.relu(z2)}[act]
+    torch.testing.assert_close(y2.float(), ref_y2, atol=1e-1, rtol=3e-2)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("D,rank,p,dres,wf32,dt", [(768, 8, 0.1, True, False, torch.bfloat16),
                                                   (768, 24, 0.0, True, False, torch.bfloat16),

@@ -161,3 +161,31 @@ def test_lmhead_dgrad_in_launch_reduction_bit_identical(monkeypatch, split):
     for _ in range(3):
         out = K.lmhead_dgrad(E, Wt, W, lab, V, stats, lse, s, 0, -1, m)
         assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("V,dtype,ignore,shift", [(50257, torch.bfloat16, -100, 128), (50272, torch.float16, 1, 0)])
+def test_lmhead_chunked_matches_whole(V, dtype, ignore, shift, monkeypatch):
+    """MIFT_LM_CHUNK (SURVEY K7's chunked head: each chunk's E consumed by its dgrad inside forward, no
+    [T, V] tensor kept): loss and gradient equal the fp32 reference and the whole-batch head, with a
+    graph-style gradient multiplier (set_head_grad_mul) and a non-unit upstream gradient."""
+    from mift.models.base import shift_labels
+    M = 4 * 128
+    h, ln, W, lab, Vp = _case(V, dtype, ignore, M=M)
+    ids = lab.view(-1, 128) if shift else lab
+    rlab = shift_labels(ids, ignore).reshape(-1) if shift else lab
+    gmul = torch.full((1,), 0.25, device="cuda")
+    res = {}
+    for chunk in ("0", "256"):
+        monkeypatch.setenv("MIFT_LM_CHUNK", chunk)
+        hx = h.clone().requires_grad_(True)
+        F.set_head_grad_mul(gmul)
+        loss = F.lm_head_xent(hx, ln, W, ids, V, ignore, need_grad=True, w_kn=W.t().contiguous(), shift=shift)
+        assert F.head_grad_mul_used()
+        F.set_head_grad_mul(None)
+        (loss * 2.0).backward()
+        res[chunk] = (float(loss.detach()), hx.grad.float())
+    rl, rg, _ = _ref(h, ln, W, rlab, V, ignore, 0.5)
+    for chunk, (l, gr) in res.items():
+        assert l == pytest.approx(float(rl), rel=3e-3), chunk
+        assert float((gr - rg).norm() / rg.norm()) < 3e-2, chunk
+    assert float((res["256"][1] - res["0"][1]).norm() / res["0"][1].norm()) < 1e-2

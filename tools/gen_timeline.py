@@ -17,11 +17,14 @@ def main():
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     tails = [i for i, r in enumerate(rows) if "decode_tail" in r["Kernel_Name"]]
+    # whole-call graph (round 5): the prefill ends with token 0's decode_tail, then new - 1 steps;
+    # older traces (one replay per step, eager prefill) have new - 1 tails per call
+    graph_call = len(tails) % new == 0 and len(tails) >= 2 * new
     reps = new - 1
     if len(tails) < 2 * reps:
         sys.exit(f"need two generate() calls in the trace ({len(tails)} decode_tail kernels)")
     last = tails[-reps:]
-    prev_end = tails[-reps - 1]
+    prev_end = tails[-reps - 2] if graph_call else tails[-reps - 1]
     per_step = last[1] - last[0]
     first_rep = last[0] - per_step + 1
     t = lambda i, k: int(rows[i][k])  # noqa: E731

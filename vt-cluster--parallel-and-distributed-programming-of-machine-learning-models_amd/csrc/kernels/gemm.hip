@@ -1477,17 +1477,24 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
 // chunks: bias, LoRA K-extension (one more k-step), pre-add, pre-activation store, forward activation,
 // residual, and the next adapter's input projection as per-column-tile fp32 slabs (proj_reduce_kernel).
 // Not for dropout (training) or activation-backward epilogues: those keep the tiled kernels.
-// LNP: A is the raw residual stream and the block applies LayerNorm(A; lnw, lnb, eps) on the fly —
+// LNM = 1: A is the raw residual stream and the block applies LayerNorm(A; lnw, lnb, eps) on the fly —
 // row statistics first (two-pass, as ln_fwd8_kernel), then every A fragment normalised and rounded
 // to 16 bits before its MFMA: the decode step's separate LN launches (13 per distilgpt2 step) go away.
-template <typename T, int BN, int NW, bool LNP>
+// LNM = 2: the LayerNorm folded into the weights (B = γ∘W rounded, lfc1 = row sums of B, lfc2 = W·β +
+// bias, fp32): the MFMAs run on the raw A fragments as soon as they land, the same two-pass row
+// statistics are taken from those registers while the matrix pipe works, and the epilogue applies
+// out = rstd·(acc − mean·lfc1) + lfc2 — no normalisation pass and no statistics barrier between the
+// loads and the first MFMA (the LNM = 1 chain cost 4-5 us per decode projection over the plain GEMM).
+template <typename T, int BN, int NW, int LNM>
 __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                               T* __restrict__ C, const T* __restrict__ A2,
                                                               const T* __restrict__ B2, int M, int N, int K, int lda,
                                                               int ldb, int ldc, EpiArgs ep, const T* __restrict__ lnw,
                                                               const T* __restrict__ lnb, float eps, int ksplit,
                                                               float* __restrict__ kws, unsigned* __restrict__ kflags,
-                                                              int pfe) {
+                                                              int pfe, const float* __restrict__ lfc1,
+                                                              const float* __restrict__ lfc2) {
+  constexpr bool LNP = LNM != 0;
   constexpr int NT = BN / 16;  // 16-column MFMA tiles per block
   constexpr int RLD = BN + 4;  // LDS row pitch (floats) of the partial tiles
   // dynamic LDS: the NW partial tiles, then (projection epilogue only) the rounded output tile
@@ -1523,12 +1530,19 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
   short8 pf_bias = short8{0, 0, 0, 0, 0, 0, 0, 0}, pf_res = pf_bias;
   const bool pf_b = PFE && pfe && ep.bias != nullptr && !ep.bias_f32;
   const bool pf_r = PFE && pfe && ep.residual != nullptr;
+  float4 pf_f1[2] = {}, pf_f2[2] = {};  // LNM = 2: this thread's chunk of lfc1 / lfc2
   if constexpr (PFE) {
     const int row = tid / CPR, c8 = (tid % CPR) * 8;
     if (tid < 64 * CPR && row < M && n0 + c8 < N) {
       if (pf_b) pf_bias = *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.bias) + n0 + c8);
       if (pf_r)
         pf_res = *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.residual) + (size_t)row * ldc + n0 + c8);
+      if constexpr (LNM == 2) {
+        pf_f1[0] = *reinterpret_cast<const float4*>(lfc1 + n0 + c8);
+        pf_f1[1] = *reinterpret_cast<const float4*>(lfc1 + n0 + c8 + 4);
+        pf_f2[0] = *reinterpret_cast<const float4*>(lfc2 + n0 + c8);
+        pf_f2[1] = *reinterpret_cast<const float4*>(lfc2 + n0 + c8 + 4);
+      }
     }
   }
   if constexpr (LNP) {
@@ -1539,8 +1553,9 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
     // normalised in place before its MFMA.  The first form re-read whole rows for the statistics,
     // one dependent load round more (12.7-13.8 us vs 6.2 us for the same GEMM without LN).
     constexpr int KSM = (1024 / 32 + NW - 1) / NW;
+    constexpr int KW = LNM == 1 ? KSM : 1;
     frag_t<T> afs[KSM][4], bfs[KSM][NT];
-    float wv[KSM][8], bv[KSM][8];
+    float wv[KW][8], bv[KW][8];
 #pragma unroll
     for (int kk = 0; kk < KSM; ++kk) {
       const int ks = w + kk * NW;
@@ -1550,8 +1565,20 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
         for (int i = 0; i < 4; ++i) afs[kk][i] = *reinterpret_cast<const frag_t<T>*>(ap[i] + k);
 #pragma unroll
         for (int j = 0; j < NT; ++j) bfs[kk][j] = *reinterpret_cast<const frag_t<T>*>(bp[j] + k);
-        load8<T>(lnw + k + fq * 8, wv[kk]);
-        load8<T>(lnb + k + fq * 8, bv[kk]);
+        if constexpr (LNM == 1) {
+          load8<T>(lnw + k + fq * 8, wv[kk]);
+          load8<T>(lnb + k + fq * 8, bv[kk]);
+        }
+      }
+    }
+    if constexpr (LNM == 2) {  // the products first: raw A against the folded weights
+#pragma unroll
+      for (int kk = 0; kk < KSM; ++kk) {
+        if (w + kk * NW >= nks) break;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bfs[kk][j], afs[kk][i], acc[i][j]);
       }
     }
     float mean[4], rstd[4];
@@ -1583,6 +1610,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
 #pragma unroll
         for (int i = 0; i < 4; ++i) lred[pass][w][i * 16 + fr] = ps[i];
       }
+      if (LNM == 2 && pass == 1) break;  // the squares are published by the partial-tile barrier below
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1593,27 +1621,29 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
         else rstd[i] = rsqrtf(t / K + eps);
       }
     }
+    if constexpr (LNM == 1) {
 #pragma unroll
-    for (int kk = 0; kk < KSM; ++kk) {
-      if (w + kk * NW >= nks) break;
+      for (int kk = 0; kk < KSM; ++kk) {
+        if (w + kk * NW >= nks) break;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        short8 raw;
-        __builtin_memcpy(&raw, &afs[kk][i], 16);
-        float x[8];
-        unpack8<T>(raw, x);
-        short8 o;
+        for (int i = 0; i < 4; ++i) {
+          short8 raw;
+          __builtin_memcpy(&raw, &afs[kk][i], 16);
+          float x[8];
+          unpack8<T>(raw, x);
+          short8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const T t = (T)((x[e] - mean[i]) * rstd[i] * wv[kk][e] + bv[kk][e]);
-          short h;
-          __builtin_memcpy(&h, &t, 2);
-          o[e] = h;
+          for (int e = 0; e < 8; ++e) {
+            const T t = (T)((x[e] - mean[i]) * rstd[i] * wv[kk][e] + bv[kk][e]);
+            short h;
+            __builtin_memcpy(&h, &t, 2);
+            o[e] = h;
+          }
+          frag_t<T> af;
+          __builtin_memcpy(&af, &o, 16);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bfs[kk][j], af, acc[i][j]);
         }
-        frag_t<T> af;
-        __builtin_memcpy(&af, &o, 16);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16<T>(bfs[kk][j], af, acc[i][j]);
       }
     }
   } else {
@@ -1655,6 +1685,28 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
   // pf: (row, c8) is this thread's prefetched chunk (ch == tid)
   auto finish = [&](int row, int c8, float* z, bool pf) {
     const int gn = n0 + c8;
+    if constexpr (LNM == 2) {  // out = rstd·(acc − mean·lfc1) + lfc2, the statistics summed in wave order
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) {
+        sm += lred[0][v][row];
+        sq += lred[1][v][row];
+      }
+      const float mu = sm / K, rs = rsqrtf(sq / K + eps);
+      float f1[8], f2[8];
+      if (pf) {
+        __builtin_memcpy(f1, pf_f1, 32);
+        __builtin_memcpy(f2, pf_f2, 32);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          f1[e] = lfc1[gn + e];
+          f2[e] = lfc2[gn + e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = rs * (z[e] - mu * f1[e]) + f2[e];
+    }
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (pf && pf_b) {
       unpack8<T>(pf_bias, bv);
@@ -1760,7 +1812,7 @@ unsigned* skinny_flags(int n) {
 template <typename T, int BN, int NW>
 void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const T* a2, const T* b2, int M, int N,
                    int K, const EpiArgs& ep, hipStream_t st, const T* lnw = nullptr, const T* lnb = nullptr,
-                   float eps = 0.f, int ksplit = 1) {
+                   float eps = 0.f, int ksplit = 1, const float* lfc1 = nullptr, const float* lfc2 = nullptr) {
   const int nb = (N + BN - 1) / BN;
   at::Tensor kwsb;
   float* kws = nullptr;
@@ -1785,27 +1837,32 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
   const int smem = RED + (ep.pw != nullptr ? OT : 0);
   static bool attr = false;
   if (!attr) {
-    if constexpr (BN == 16 && NW == 8)
-      (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, true>,
+    if constexpr (BN == 16 && NW == 8) {
+      (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, 1>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, RED + OT);
-    (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, false>,
+      (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, RED + OT);
+    }
+    (void)hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, BN, NW, 0>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, RED + OT);
     attr = true;
   }
-  if (lnw != nullptr) {
-    // the LN prologue holds a wave's whole K range in registers: the 16-column, 8-wave form only
-    if constexpr (BN == 16 && NW == 8)
-      hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, true>), dim3(nb), dim3(NW * 64), smem, st,
-                         (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
-                         (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, lnw, lnb, eps, 1,
-                         (float*)nullptr, (unsigned*)nullptr, pfe);
-    else
+  if (lnw != nullptr || lfc1 != nullptr) {
+    // the LN prologue / folded LN holds a wave's whole K range in registers: the 16-column, 8-wave form only
+    if constexpr (BN == 16 && NW == 8) {
+      auto kern = lfc1 != nullptr ? gemm_skinny_kernel<T, BN, NW, 2> : gemm_skinny_kernel<T, BN, NW, 1>;
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(NW * 64), smem, st, (const T*)a.data_ptr(), (const T*)b.data_ptr(),
+                         (T*)c.data_ptr(), a2, b2, M, N, K, (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx,
+                         lnw, lnb, eps, 1, (float*)nullptr, (unsigned*)nullptr, pfe, lfc1, lfc2);
+    } else {
       TORCH_CHECK(false, "gemm_skinny: LN prologue needs the 16-column 8-wave form");
-  } else
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, false>), dim3(nb * ksplit), dim3(NW * 64), smem, st,
+    }
+  } else {
+    hipLaunchKernelGGL((gemm_skinny_kernel<T, BN, NW, 0>), dim3(nb * ksplit), dim3(NW * 64), smem, st,
                        (const T*)a.data_ptr(), (const T*)b.data_ptr(), (T*)c.data_ptr(), a2, b2, M, N, K,
                        (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), epx, (const T*)nullptr,
-                       (const T*)nullptr, 0.f, ksplit, kws, kflags, pfe);
+                       (const T*)nullptr, 0.f, ksplit, kws, kflags, pfe, (const float*)nullptr, (const float*)nullptr);
+  }
   if (ep.pw != nullptr)
     hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
                        (const float*)epx.pws, nb, M, PW, ep.palpha, (T*)ep.pout);
@@ -2314,6 +2371,39 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
 // (no normalised copy of x, no LN launch).  The caller checks mift_gemm_ln_ok (else LN + gemm_nt).
 bool mift_gemm_ln_ok(int64_t M, int64_t N, int64_t K) { return M >= 1 && M <= 64 && N % 16 == 0 && N <= 4096 &&
                                                                K % 64 == 0 && K <= 1024; }
+
+// out [M, N] = act(rstd·(x·wfᵀ − mean·c1) + c2) = act(LayerNorm(x; γ, β) · wᵀ + bias) with wf = γ∘w (x's
+// dtype), c1 = row sums of wf and c2 = w·β + bias (fp32 [N]) prepared once by the caller
+// (mift.ops.fused._ln_fold): the skinny kernel's LNM = 2 form (decode projections, M <= 64).
+at::Tensor mift_gemm_ln_fold(const at::Tensor& x, const at::Tensor& wf, const at::Tensor& c1, const at::Tensor& c2,
+                             double eps, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && wf.is_cuda() && x.dim() == 2 && wf.dim() == 2 && x.size(1) == wf.size(1),
+              "gemm_ln_fold: x [M,K], wf [N,K]");
+  TORCH_CHECK(x.stride(1) == 1 && wf.stride(1) == 1 && x.stride(0) % 8 == 0 && wf.stride(0) % 8 == 0,
+              "gemm_ln_fold: layouts");
+  const int M = x.size(0), K = x.size(1), N = wf.size(0);
+  TORCH_CHECK(x.scalar_type() == wf.scalar_type(), "gemm_ln_fold: wf of x's dtype");
+  TORCH_CHECK(c1.scalar_type() == at::kFloat && c2.scalar_type() == at::kFloat && c1.is_contiguous() &&
+                  c2.is_contiguous() && c1.numel() == N && c2.numel() == N,
+              "gemm_ln_fold: c1 / c2 fp32 [N]");
+  TORCH_CHECK(mift_gemm_ln_ok(M, N, K), "gemm_ln_fold: M <= 64, N % 16 == 0, N <= 4096, K % 64 == 0, K <= 1024");
+  TORCH_CHECK(act == ACT_NONE || act == ACT_GELU_TANH || act == ACT_RELU || act == ACT_GELU_ERF,
+              "gemm_ln_fold: forward act");
+  at::Tensor c = at::empty({M, N}, x.options());
+  EpiArgs ep{};
+  ep.alpha = 1.f;
+  ep.act = (int)act;
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  if (x.scalar_type() == at::kBFloat16)
+    launch_skinny<bf16, 16, 8>(x, wf, c, nullptr, nullptr, M, N, K, ep, st, nullptr, nullptr, (float)eps, 1,
+                               c1.data_ptr<float>(), c2.data_ptr<float>());
+  else {
+    TORCH_CHECK(x.scalar_type() == at::kHalf, "gemm_ln_fold: bf16/fp16");
+    launch_skinny<fp16, 16, 8>(x, wf, c, nullptr, nullptr, M, N, K, ep, st, nullptr, nullptr, (float)eps, 1,
+                               c1.data_ptr<float>(), c2.data_ptr<float>());
+  }
+  return c;
+}
 
 std::vector<at::Tensor> mift_gemm_ln(const at::Tensor& x, const at::Tensor& ln_w, const at::Tensor& ln_b, double eps,
                                      const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,

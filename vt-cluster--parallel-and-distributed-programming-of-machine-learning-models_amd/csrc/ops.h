@@ -100,6 +100,8 @@ bool mift_gemm_ln_ok(int64_t M, int64_t N, int64_t K);
 std::vector<at::Tensor> mift_gemm_ln(const at::Tensor& x, const at::Tensor& ln_w, const at::Tensor& ln_b, double eps,
                                      const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
                                      bool want_preact);
+at::Tensor mift_gemm_ln_fold(const at::Tensor& x, const at::Tensor& wf, const at::Tensor& c1, const at::Tensor& c2,
+                             double eps, int64_t act);
 void mift_decode_tail(const at::Tensor& logits, int64_t V, at::Tensor& done, at::Tensor& ids, at::Tensor& out,
                       at::Tensor& col, at::Tensor& pos, at::Tensor& t, int64_t fill, int64_t pad, int64_t eos);
 at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
@@ -109,6 +111,7 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
 #define MIFT_BIND_MORE(m) \
   m.def("gemm_ln_ok", &mift_gemm_ln_ok, "shapes the LN-prologue skinny GEMM takes"); \
   m.def("gemm_ln", &mift_gemm_ln, "act(LN(x) w^T + bias) for M <= 64 rows (decode), LN applied in the GEMM"); \
+  m.def("gemm_ln_fold", &mift_gemm_ln_fold, "act(rstd (x wf^T - mean c1) + c2): LN folded into the weights (decode)"); \
   m.def("decode_tail", &mift_decode_tail, "greedy decode step tail: argmax, pad/eos, next ids, out/col/pos/t advance"); \
   m.def("decode_attn", &mift_decode_attn, "single-token attention over a KV cache; appends k/v at t (left padding: start; prompt gap: plen, gend)"); \
   m.def("lora_proj", &mift_lora_proj, "out[M,32] = alpha*drop(x)@w^T (tall-skinny MFMA)"); \

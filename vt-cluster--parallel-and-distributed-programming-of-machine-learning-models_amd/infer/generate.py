@@ -16,14 +16,16 @@ the ``decode_attn`` HIP kernel, which appends the new K/V in the same
 launch, and the LM-head logits are the hand-written MFMA GEMM (``gemm_nt``).
 No library GEMM and no SDPA run on the GPU path.
 
-Decode steps are replayed from ONE hipGraph (``_DecodeGraph``; ``MIFT_GEN_GRAPH=0`` disables): a
-step is ~45 kernels of a few microseconds each, so eagerly it was host-launch bound (0.62 ms per
-step for distilgpt2 at batch 64).  Everything a step varies lives on the
-device — the cache position (``decode_attn`` reads it from an int32 tensor), the positions, the
-finished-row flags and the output column — and advances inside the graph, so one capture serves
-every step and, cached per (model, batch, prompt length, budget), every later call of the same
-shape.  HF's stop-when-all-finished rule is applied afterwards: the steps past the last row's EOS
-only produce pad tokens and are trimmed (no per-step host sync).
+A whole call — prefill, token 0 and every decode step — is replayed from ONE hipGraph
+(``_DecodeGraph``; ``MIFT_GEN_GRAPH=0`` disables): a step is ~34 kernels of a few microseconds each, so
+eagerly it was host-launch bound (0.62 ms per step for distilgpt2 at batch 64),
+and the eager prefill spent 1.67 ms of span on 0.61 ms of kernels (round 5).  Everything a step
+varies lives on the device — the cache position (``decode_attn`` reads it from an int32 tensor), the
+positions, the finished-row flags and the output column — and advances inside the graph, so the
+steps are identical captures and, cached per (model, batch, prompt length, budget), one graph serves
+every later call of the same shape (its ids and prompt lengths are copied into static inputs).  HF's
+stop-when-all-finished rule is applied afterwards: the steps past the last row's EOS only produce
+pad tokens and are trimmed (no per-step host sync).
 
 Left-padded batches: the prefill runs every prompt RIGHT-aligned to position 0
 (row b's tokens ``ids[b, start_b:]`` then padding) so the flash kernel's
@@ -125,7 +127,14 @@ def _heads(model):
 
 
 class _DecodeGraph:
-    """One captured greedy decode step over static device state (see the module docstring)."""
+    """One greedy generate() call of a fixed shape over static device state: the prefill, token 0's
+    argmax / bookkeeping and every decode step, captured as ONE hipGraph (see the module docstring).
+
+    The first call of a shape runs the same sequence eagerly (its result is that call's output) and
+    then captures it; later calls copy their ids / prompt lengths into the static inputs and replay
+    once.  The prefill was ~90 host-issued kernels with 10-20 us of launch gap each (1.67 ms span for
+    0.61 ms of kernels at batch 64, ``profiles/r5/gen_timeline_r5k.txt``) and every decode step one
+    replay of its own."""
 
     def __init__(self, model, B, S0, max_new, padded, pad, eos, fill, H, hd, dtype, dev):
         self.key = (B, S0, max_new, padded, pad, eos, fill)
@@ -135,7 +144,11 @@ class _DecodeGraph:
         L = len(model.blocks())
         self.cache = KVCache(L, B, H, S0 + max_new, hd, dtype, dev)
         self.B, self.S0, self.H, self.hd, self.fill, self.pad, self.eos = B, S0, H, hd, fill, pad, eos
-        self.nxt = torch.zeros(B, dtype=torch.long, device=dev)
+        self.max_new, self.padded = max_new, padded
+        self.in_ids = torch.zeros(B, S0, dtype=torch.long, device=dev)  # static inputs of a call
+        self.in_lens = torch.zeros(B, dtype=torch.long, device=dev)
+        self.lens_pin = torch.zeros(B, dtype=torch.long, pin_memory=True)  # host side of in_lens' upload
+        self.lens_ev = None
         self.ids = torch.zeros(B, 1, dtype=torch.long, device=dev)  # this step's input token per row
         self.done = torch.zeros(B, dtype=torch.bool, device=dev)
         self.t = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -145,11 +158,42 @@ class _DecodeGraph:
         self.plen = torch.zeros(B, dtype=torch.int32, device=dev) if padded else None
         self.graph = None
 
+    def prefill(self, model):
+        """Prompts (static in_ids / in_lens) through the model, K/V rows [0, S0) of every layer cached,
+        then token 0: argmax of each row's last prompt position through ``decode_tail`` with the state
+        set so that it leaves t = S0, pos = len, col = 1 (HF: a row is finished once it emits EOS)."""
+        from ..ops import kernels as K
+        B, S0, H, hd = self.B, self.S0, self.H, self.hd
+        dev = self.in_ids.device
+        ar = torch.arange(S0, device=dev)
+        lens = self.in_lens
+        if self.padded:  # right-align every prompt to position 0 (see generate)
+            self.plen.copy_(lens)
+            src = (ar[None, :] + (S0 - lens)[:, None]).clamp(max=S0 - 1)
+            ids_r = torch.where(ar[None, :] < lens[:, None], torch.gather(self.in_ids, 1, src),
+                                torch.full_like(self.in_ids, self.fill))
+        else:
+            ids_r = self.in_ids
+        h = model.embed_at(ids_r, ar[None, :].expand(B, S0).contiguous())
+        h = _run_blocks(model, h, lambda li: _prefill_attn(self.cache, li, B, S0, H, hd, self.plen, True), True)
+        if self.padded:
+            last = (lens - 1).clamp(min=0)
+            h_last = torch.gather(h, 1, last[:, None, None].expand(B, 1, h.shape[-1]))
+        else:
+            h_last = h[:, -1:]
+        logits = model.head_logits(h_last)[:, -1]
+        self.done.zero_()
+        self.col.zero_()
+        self.out.zero_()
+        self.t.fill_(S0 - 1)
+        self.pos.copy_((lens - 1)[:, None])
+        K.decode_tail(logits, logits.shape[-1], self.done, self.ids, self.out, self.col, self.pos, self.t, self.fill,
+                      self.pad, self.eos)
+
     def step(self, model):
-        """One decode step on the static state (eager, or recorded during capture).  The greedy tail —
-        argmax, pad for finished rows, the output column, EOS flags, the next input ids and the
-        position / column / cache-position advance — is ONE kernel (``decode_tail``; it was ~12 torch
-        kernels per step)."""
+        """One decode step on the static state.  The greedy tail — argmax, pad for finished rows, the
+        output column, EOS flags, the next input ids and the position / column / cache-position
+        advance — is ONE kernel (``decode_tail``; it was ~12 torch kernels per step)."""
         from ..ops import kernels as K
         B, H, hd = self.B, self.H, self.hd
         h = model.embed_at(self.ids, self.pos)
@@ -159,36 +203,71 @@ class _DecodeGraph:
         K.decode_tail(logits, logits.shape[-1], self.done, self.ids, self.out, self.col, self.pos, self.t, self.fill,
                       self.pad, self.eos)
 
-    def run(self, model, nsteps):
-        if nsteps <= 0:
-            return
-        i = 0
-        if self.graph is None:
-            self.step(model)  # eager warm-up (first launch of every kernel module), then capture
-            i = 1
-            if nsteps > 1:
-                # the capture must rebuild every cached LoRA operand pack INSIDE the graph (each replay then
-                # re-packs from the live adapter weights); without this the eager step's packs, built at the
-                # same arena version, are baked in and a later prefill that replaces them leaves the replays
-                # reading freed memory
-                from ..ops.fused import invalidate_packs
-                invalidate_packs(model)
-                g = torch.cuda.CUDAGraph()
-                was = gc.isenabled()
-                gc.collect()
-                gc.disable()  # no finalizers of device objects inside the capture (train/graph.py)
-                try:
-                    with torch.cuda.graph(g):
-                        self.step(model)
-                finally:
-                    if was:
-                        gc.enable()
-                self.graph = g
-        for _ in range(i, nsteps):
+    def call(self, model):
+        self.prefill(model)
+        for _ in range(self.max_new - 1):
+            self.step(model)
+
+    def run(self, model, input_ids, lens):
+        """Tokens [B, max_new] of one call (static output; the caller copies it out).  ``lens``: host
+        int64 prompt lengths (uploaded through a pinned buffer)."""
+        self.in_ids.copy_(input_ids)
+        if self.lens_ev is not None:
+            self.lens_ev.synchronize()  # the previous call's upload has read the pinned buffer
+        self.lens_pin.copy_(lens)
+        self.in_lens.copy_(self.lens_pin, non_blocking=True)
+        self.lens_ev = torch.cuda.Event()
+        self.lens_ev.record()
+        if self.graph is not None:
             self.graph.replay()
+            return self.out
+        self.call(model)  # first call of this shape: eager (first launch of every kernel module) ...
+        # ... then the capture, which must rebuild every cached LoRA operand pack INSIDE the graph (each
+        # replay then re-packs from the live adapter weights); without this the eager pass's packs, built
+        # at the same arena version, are baked in and a later call that replaces them leaves the replays
+        # reading freed memory (ADVICE r4).  The eager pass's tokens are kept aside: the capture itself
+        # runs nothing, but it must not race the copy-out.
+        toks = self.out.clone()
+        from ..ops.fused import invalidate_packs
+        invalidate_packs(model)
+        g = torch.cuda.CUDAGraph()
+        was = gc.isenabled()
+        gc.collect()
+        gc.disable()  # no finalizers of device objects inside the capture (train/graph.py)
+        try:
+            with torch.cuda.graph(g):
+                self.call(model)
+        finally:
+            if was:
+                gc.enable()
+        self.graph = g
+        return toks
 
 
 _GRAPHS = {}
+_PINNED = {}
+
+
+def _pinned(shape, dtype):
+    """A reusable page-locked host buffer (pageable copies cost ~100 us each way on this stack:
+    profiles/r5/gen_timeline_r5m.txt)."""
+    key = (tuple(shape), dtype)
+    b = _PINNED.get(key)
+    if b is None:
+        if len(_PINNED) >= 16:
+            _PINNED.pop(next(iter(_PINNED)))
+        b = _PINNED[key] = torch.empty(shape, dtype=dtype, pin_memory=torch.cuda.is_available())
+    return b
+
+
+def _to_host(t):
+    """int64 host copy of a (small) tensor through a pinned buffer (one DMA, one stream sync)."""
+    if t.device.type != "cuda":
+        return t.to(torch.long)
+    b = _pinned(t.shape, t.dtype)
+    b.copy_(t, non_blocking=True)
+    torch.cuda.current_stream(t.device).synchronize()
+    return b.to(torch.long)
 
 
 def _arena_version(model):
@@ -226,13 +305,18 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
     pad = getattr(cfg, "pad_token_id", eos) if pad_token_id is None else pad_token_id
     if max_length is not None:
         max_new_tokens = max(0, min(max_new_tokens, max_length - S0))
+    # the mask's checks run on the host: one small device-to-host copy instead of a chain of tiny
+    # kernels and syncs ahead of the (graph-replayed) call
     if attention_mask is None:
-        attention_mask = torch.ones_like(input_ids)
-    lens = attention_mask.sum(1)
-    start = (S0 - lens)
-    if bool((attention_mask != (torch.arange(S0, device=dev)[None, :] >= start[:, None]).long()).any()):
-        raise ValueError("generate expects left padding (HF padding_side='left')")
-    padded = bool((start > 0).any())
+        lens_h = torch.full((B,), S0, dtype=torch.long)
+        padded = False
+    else:
+        mask_h = _to_host(attention_mask)
+        lens_h = mask_h.sum(1)
+        if bool((mask_h != (torch.arange(S0)[None, :] >= (S0 - lens_h)[:, None]).long()).any()):
+            raise ValueError("generate expects left padding (HF padding_side='left')")
+        padded = bool((lens_h < S0).any())
+    lens = lens_h.to(dev)
     plen = lens.to(torch.int32).contiguous() if padded else None
     fused = model._use_fused(input_ids)
     H, hd = _heads(model)
@@ -240,18 +324,14 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
     dtype = model.tied_embedding().dtype
     vocab = model.tied_embedding().shape[0]
     fill = pad if pad is not None and 0 <= pad < vocab else 0
-    dg = None
     if (fused and dev.type == "cuda" and max_new_tokens > 2 and os.environ.get("MIFT_GEN_GRAPH", "1") != "0"
             and S0 + max_new_tokens <= 16384):
         dg = _decode_graph(model, (B, S0, max_new_tokens, padded, pad, eos, fill, H, hd, dtype, dev))
-        cache = dg.cache
-        if padded:
-            dg.plen.copy_(plen)
-            plen = dg.plen
-    else:
-        cache = KVCache(L, B, H, S0 + max_new_tokens, hd, dtype, dev)
+        return _graphed_generate(dg, model, input_ids, lens_h, max_new_tokens, eos)
+    cache = KVCache(L, B, H, S0 + max_new_tokens, hd, dtype, dev)
 
     # prefill over right-aligned prompts: row b = ids[b, start_b:] then padding, positions 0..S0-1
+    start = S0 - lens
     ar = torch.arange(S0, device=dev)
     # filler after each right-aligned prompt / input of a finished row (``fill`` above): any id INSIDE
     # the embedding table.  Filler K/V are masked (kv_len, the decode gap) but still multiplied by
@@ -269,8 +349,6 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
     h_last = torch.gather(h, 1, last[:, None, None].expand(B, 1, h.shape[-1])) if padded else h[:, -1:]
     logits = model.head_logits(h_last)
     nxt = logits[:, -1].float().argmax(-1)
-    if dg is not None:
-        return _graphed_decode(dg, model, input_ids, nxt, lens, max_new_tokens, pad, eos)
     out = [input_ids]
     done = torch.zeros(B, dtype=torch.bool, device=dev)
     for i in range(max_new_tokens):
@@ -288,20 +366,10 @@ def generate(model, input_ids, attention_mask=None, max_new_tokens=16, eos_token
     return torch.cat(out, 1)
 
 
-def _graphed_decode(dg, model, input_ids, nxt, lens, max_new_tokens, pad, eos):
-    """Token 0 from the prefill, tokens 1.. from graph replays; HF's early stop applied afterwards."""
-    done = torch.zeros_like(dg.done) if eos is None else (nxt == eos)
-    dg.nxt.copy_(nxt)
-    dg.done.copy_(done)
-    dg.ids.copy_(torch.where(done, torch.full_like(nxt, dg.fill), nxt)[:, None])
-    dg.out.zero_()
-    dg.out[:, 0] = nxt
-    dg.t.fill_(dg.S0)
-    dg.pos.copy_(lens[:, None])
-    dg.col.fill_(1)
-    dg.run(model, max_new_tokens - 1)
-    toks = dg.out.clone()
-    if eos is not None:
+def _graphed_generate(dg, model, input_ids, lens, max_new_tokens, eos):
+    """The whole call from one graph replay (or its eager first run); HF's early stop applied after."""
+    toks = dg.run(model, input_ids, lens).clone()
+    if eos is not None and eos >= 0:  # (a negative id is never emitted)
         # HF stops after the step in which the last unfinished row emitted EOS
         hit = toks == eos
         if bool(hit.any(1).all()):

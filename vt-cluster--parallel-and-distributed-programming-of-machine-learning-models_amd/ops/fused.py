@@ -452,11 +452,38 @@ def _infer_ln_gemm(x, ln, lin):
     return x2, w
 
 
+def _ln_fold(ln, lin, w):
+    """(wf, c1, c2) of LayerNorm(x; γ, β)·wᵀ + bias with the LN folded into the weights: wf = γ∘w rounded
+    to w's dtype, c1 = Σ_k wf[:, k] and c2 = w·β + bias in fp32 (K.gemm_ln_fold).  Cached on the linear,
+    keyed by the storage and version counters of every operand (rebuilt after any in-place update)."""
+    b = lin.bias
+    key = (w.data_ptr(), w._version, ln.weight.data_ptr(), ln.weight._version, ln.bias.data_ptr(), ln.bias._version,
+           None if b is None else (b.data_ptr(), b._version))
+    c = getattr(lin, "_mift_lnfold", None)
+    if c is None or c[0] != key:
+        g, beta = ln.weight.detach().float(), ln.bias.detach().float()
+        wf = (w.float() * g[None, :]).to(w.dtype).contiguous()
+        c1 = wf.float().sum(1).contiguous()
+        c2 = (w.float() @ beta + (b.detach().float() if b is not None else 0.0)).contiguous()
+        c = (key, wf, c1, c2)
+        lin._mift_lnfold = c
+    return c[1:]
+
+
+def _gemm_ln(x2, ln, lin, w, act=0):
+    """Decode projection of LN(x): the folded form (K.gemm_ln_fold) unless MIFT_LN_FOLD=0 (read per call:
+    the LN-prologue form, K.gemm_ln).  Both are M <= 64 skinny-GEMM launches."""
+    if os.environ.get("MIFT_LN_FOLD", "1") != "0":
+        wf, c1, c2 = _ln_fold(ln, lin, w)
+        return K.gemm_ln_fold(x2, wf, c1, c2, ln.eps, act=act)
+    return K.gemm_ln(x2, ln.weight, ln.bias, ln.eps, w, lin.bias, act=act)
+
+
 def ln_linear(x, ln, lin, lora_seed=0, training=True, link=None):
     fast = _infer_ln_gemm(x, ln, lin)
     if fast is not None:  # decode: one launch instead of LN + GEMM
         x2, w = fast
-        return K.gemm_ln(x2, ln.weight, ln.bias, ln.eps, w, lin.bias).view(*x.shape[:-1], w.shape[0])
+        return _gemm_ln(x2, ln, lin, w).view(*x.shape[:-1], w.shape[0])
     return LnLinear.apply(x, ln.weight, ln.bias, lin, ln.eps, lora_seed, training, link, *lin.lora_params())
 
 
@@ -570,7 +597,7 @@ def mlp(h, ln, fc1, fc2, act, p, seed, seed_l1=0, seed_l2=0, training=True, hand
     fast = _infer_ln_gemm(h, ln, fc1)
     if fast is not None and not training:  # decode: LN inside fc1's skinny GEMM, no pre-activation store
         h2, w1 = fast
-        f = K.gemm_ln(h2, ln.weight, ln.bias, ln.eps, w1, fc1.bias, act=act)
+        f = _gemm_ln(h2, ln, fc1, w1, act=act)
         lo2 = fc2.lora_ops(h.dtype) if fc2.lora_params() else None
         T2 = lo2.forward(f, seed_l2, False) if lo2 is not None else None
         out = K.gemm(f, fc2.w_nk(), fc2.bias, T2, lo2.B32 if lo2 else None, residual=h2)
@@ -613,24 +640,47 @@ class LMHeadXent(torch.autograd.Function):
         a, mean, rstd = K.layer_norm_fwd(h2, ln_w, ln_b, eps)
         lab = labels.reshape(-1).contiguous()
         ign = int(ignore_index) if ignore_index >= 0 else -1  # e.g. OPT ignores the pad id, a real entry
-        outs = K.lmhead_fwd(a, w_nk, lab, V, shift, ign, _lm_ws(a.device))
-        E, stats, lse, total = outs[0], outs[1], outs[2], outs[5]
-        if need_grad:
-            ctx.save_for_backward(h2, mean, rstd, ln_w, E, stats, lse, lab)
         ctx.shp, ctx.w_nk, ctx.w_kn, ctx.V, ctx.shift, ctx.ign = shp, w_nk, w_kn, V, shift, ign
         ctx.hand = getattr(h, "_mift_hand", None)  # the last block's mlp dropout-bwd rides on the final LN's
         ctx.gmul = _HEAD_GMUL[0]
         if ctx.gmul is not None:
             _HEAD_GMUL[1] = True
+        C = _lm_chunk(a.shape[0], shift) if need_grad else 0
+        if C:
+            # chunked: per C-row chunk the forward's E [C, V_pad] is consumed by that chunk's
+            # dgrad at once (g = 1; the upstream gradient scales dX in backward), so no [T, V] tensor
+            # lives past its chunk and the chunk's E can stay in the Infinity Cache
+            w_kn_ = w_kn if w_kn is not None else w_nk.t().contiguous()
+            one = _lm_one(a.device)
+            ws = _lm_ws(a.device)
+            dx, total = [], None
+            for r0 in range(0, a.shape[0], C):
+                ac, lc = a[r0:r0 + C], lab[r0:r0 + C]
+                outs = K.lmhead_fwd(ac, w_nk, lc, V, shift, ign, ws)
+                dx.append(K.lmhead_dgrad(outs[0], w_kn_, w_nk, lc, V, outs[1], outs[2], one, shift, ign, None))
+                total = outs[5] if total is None else total + outs[5]
+            ctx.save_for_backward(h2, mean, rstd, ln_w, torch.cat(dx))
+            ctx.chunked = True
+            return total.view(())
+        outs = K.lmhead_fwd(a, w_nk, lab, V, shift, ign, _lm_ws(a.device))
+        E, stats, lse, total = outs[0], outs[1], outs[2], outs[5]
+        if need_grad:
+            ctx.save_for_backward(h2, mean, rstd, ln_w, E, stats, lse, lab)
+        ctx.chunked = False
         return total.view(())
 
     @staticmethod
     def backward(ctx, g):
-        h2, mean, rstd, ln_w, E, stats, lse, lab = ctx.saved_tensors
-        w_kn = ctx.w_kn if ctx.w_kn is not None else ctx.w_nk.t().contiguous()
-        g1 = g.reshape(1)
-        da = K.lmhead_dgrad(E, w_kn, ctx.w_nk, lab, ctx.V, stats, lse, g1 if g1.dtype == torch.float32 else g1.float(),
-                            ctx.shift, ctx.ign, ctx.gmul)
+        if ctx.chunked:
+            h2, mean, rstd, ln_w, dx1 = ctx.saved_tensors
+            sc = g.reshape(1).float() if ctx.gmul is None else g.reshape(1).float() * ctx.gmul
+            da = (dx1.float() * sc).to(dx1.dtype)  # unit-gradient dX, scaled once in fp32
+        else:
+            h2, mean, rstd, ln_w, E, stats, lse, lab = ctx.saved_tensors
+            w_kn = ctx.w_kn if ctx.w_kn is not None else ctx.w_nk.t().contiguous()
+            g1 = g.reshape(1)
+            da = K.lmhead_dgrad(E, w_kn, ctx.w_nk, lab, ctx.V, stats, lse,
+                                g1 if g1.dtype == torch.float32 else g1.float(), ctx.shift, ctx.ign, ctx.gmul)
         dh = _ln_bwd(ctx.hand, da, h2, ln_w, mean, rstd, None)
         return dh.view(ctx.shp), None, None, None, None, None, None, None, None, None, None
 
@@ -672,6 +722,29 @@ class LMHeadXentBlas(torch.autograd.Function):
 
 
 _LM_WS = {}
+_LM_ONE = {}
+
+
+def _lm_chunk(M, shift):
+    """Rows per chunk of the chunked head (MIFT_LM_CHUNK, read per call; 0 = whole batch, the default): a
+    multiple of the sequence length when the labels are unshifted ids, and only when it actually splits M.
+    Opt-in for memory-limited runs: the whole-batch head streams its 824 MB E once through HBM, which on
+    MI355X costs less than the chunks' smaller grids and split-K slabs — distilgpt2 step 4.90 ms whole vs
+    5.03 / 5.42 / 6.00 at 4096- / 2048- / 1024-row chunks (profiles/r5/step_ab_lm_chunk.json)."""
+    c = int(os.environ.get("MIFT_LM_CHUNK", "0"))
+    if c <= 0 or c >= M:
+        return 0
+    if shift:
+        c = max(shift, c // shift * shift)
+    return c if c < M else 0
+
+
+def _lm_one(dev):
+    """A device fp32 1.0 (the chunked head's dgrad runs at unit upstream gradient)."""
+    t = _LM_ONE.get(dev)
+    if t is None:
+        t = _LM_ONE[dev] = torch.ones(1, dtype=torch.float32, device=dev)
+    return t
 _HEAD_GMUL = [None, False]  # (multiplier tensor, consumed by a head since set_head_grad_mul)
 
 

@@ -43,6 +43,12 @@ def gemm_ln(x, ln_w, ln_b, eps, w, bias=None, act=0, want_preact=False):
     return (y, pre) if want_preact else y
 
 
+def gemm_ln_fold(x, wf, c1, c2, eps, act=0):
+    """act(LayerNorm(x) @ w.T + bias) with the LN folded into the weights (wf = γ∘w, c1 = wf row sums,
+    c2 = w·β + bias, fp32): rstd·(x @ wf.T − mean·c1) + c2 in one launch (M <= 64, decode)."""
+    return C().gemm_ln_fold(x, wf, c1, c2, float(eps), int(act))
+
+
 def lora_proj(x, w32, alpha=1.0, p=0.0, seed=0, rows=32):
     """[M,32] = alpha * dropout(x) @ w32.T   (w32: [32, K]; only its first ``rows`` rows may be non-zero)."""
     return C().lora_proj(x, w32, float(alpha), float(p), int(seed), int(rows))
