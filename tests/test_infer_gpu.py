@@ -181,3 +181,60 @@ def test_graphed_decode_matches_eager(name, monkeypatch):
     monkeypatch.setenv("MIFT_GEN_GRAPH", "1")
     g = G.generate(m, same, attention_mask=msk, max_new_tokens=12, eos_token_id=eos)
     assert e.shape[1] <= same.shape[1] + 4 and torch.equal(e, g), (e.shape, g.shape)
+
+
+@pytest.mark.parametrize("hd,dt", [(64, torch.bfloat16), (80, torch.float16), (128, torch.bfloat16)])
+def test_kv_store_matches_strided_copies(hd, dt):
+    """kv_store (prefill, one launch) writes exactly the rows the two strided cache copies wrote."""
+    from mift.ops import kernels as K
+    torch.manual_seed(2)
+    B, H, S, Tmax = 3, 5, 37, 50
+    d = H * hd
+    qkv = torch.randn(B * S, 3 * d, device="cuda").to(dt)
+    kc = torch.randn(B, H, Tmax, hd, device="cuda").to(dt)
+    vc = torch.randn(B, H, Tmax, hd, device="cuda").to(dt)
+    kr, vr = kc.clone(), vc.clone()
+    q3 = qkv.view(B, S, 3 * d)
+    kr[:, :, :S].copy_(q3[..., d:2 * d].view(B, S, H, hd).transpose(1, 2))
+    vr[:, :, :S].copy_(q3[..., 2 * d:].view(B, S, H, hd).transpose(1, 2))
+    K.kv_store(qkv, kc, vc, S)
+    assert torch.equal(kc, kr) and torch.equal(vc, vr)
+
+
+def test_graphed_generate_follows_adapter_updates(monkeypatch):
+    """the cached whole-call decode graph must not replay stale LoRA operands.  OPT with
+    adapters on q / v (one multi-adapter K-extension) and fc1: generate (capture + replay), change the
+    adapters in place through the arena as an optimizer step does (version bump), generate again —
+    every graphed call equals the eager path (MIFT_GEN_GRAPH=0) on the weights of that moment."""
+    from mift import lora as L
+    from mift.apps.gen_probe import distinct_prompts
+    from mift.infer import generate as G
+    from mift.models.opt import OPTConfig, OPTForCausalLM
+    m = OPTForCausalLM(OPTConfig(vocab_size=1000, hidden_size=320, num_hidden_layers=2, ffn_dim=1280,
+                                 num_attention_heads=4, max_position_embeddings=128), dtype=torch.float16,
+                       device="cuda").init_weights(3)
+    L.inject(m, L.LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["q_proj", "v_proj", "fc1"]))
+    arena = L.LoraArena(m)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    with torch.no_grad():
+        arena.param.copy_(torch.randn(arena.param.shape, device="cuda", generator=g) * 0.2)
+    arena.bump()
+    m.eval()
+    ids, mask = distinct_prompts(16, 1000, 1, "cuda")
+
+    def both():
+        monkeypatch.setenv("MIFT_GEN_GRAPH", "0")
+        e = G.generate(m, ids, attention_mask=mask, max_new_tokens=10, eos_token_id=-1)
+        monkeypatch.setenv("MIFT_GEN_GRAPH", "1")
+        g1 = G.generate(m, ids, attention_mask=mask, max_new_tokens=10, eos_token_id=-1)
+        g2 = G.generate(m, ids, attention_mask=mask, max_new_tokens=10, eos_token_id=-1)
+        return e, g1, g2
+
+    e0, a0, b0 = both()
+    assert torch.equal(e0, a0) and torch.equal(e0, b0)
+    with torch.no_grad():  # an "optimizer step": new adapter values in place, version bumped
+        arena.param.add_(torch.randn(arena.param.shape, device="cuda", generator=g) * 0.5)
+    arena.bump()
+    e1, a1, b1 = both()
+    assert torch.equal(e1, a1) and torch.equal(e1, b1)
+    assert not torch.equal(e0, e1)  # the adapters matter: the update changed the tokens

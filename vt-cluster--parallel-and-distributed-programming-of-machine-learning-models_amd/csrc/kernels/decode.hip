@@ -31,10 +31,12 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ 
   // t_dev: the position lives on the device (graph-replayed decode steps advance it in-graph)
   const int t = t_dev ? t_dev[0] : t_arg;
   constexpr int G = 256 / HD;  // key groups in the P·V pass
+  constexpr int NC = HD / 8;   // 16-B pieces per K / V row
   extern __shared__ float sm[];
   float* qs = sm;              // [HD]
   float* red = qs + HD;        // [G*HD] (also used for the block reductions)
-  float* sc = red + G * HD;    // [t+1]
+  T* vs = reinterpret_cast<T*>(red + G * HD);  // [256][HD]: V rows of keys 0..255 (16-B aligned)
+  float* sc = reinterpret_cast<float*>(vs + 256 * HD);  // [t+1]
   const int bh = blockIdx.x, b = bh / H, h = bh % H, tid = threadIdx.x;
   const int64_t ld = 3LL * H * HD;
   const T* qg = qkv + (int64_t)b * ld + h * HD;
@@ -42,26 +44,52 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ 
   const T* vg = qg + 2LL * H * HD;
   T* kcb = kc + (int64_t)bh * Tmax * HD;
   T* vcb = vc + (int64_t)bh * Tmax * HD;
+  const int s0 = start ? start[b] : 0;
+  const int g0 = plen ? plen[b] : gend;  // masked gap [g0, gend)
+  // Every global read of keys 0..255 is issued here, before the first barrier: thread j holds key j's
+  // K row in registers and stages its V row in LDS, so a short context (every decode step of the
+  // distilgpt2 probe) pays one memory latency instead of three dependent ones (q -> K rows -> V rows).
+  // Key t (the new token) comes from the qkv row, never from the cache written in this launch.
+  const int j0 = tid;
+  const bool live0 = j0 <= t && j0 >= s0 && (j0 < g0 || j0 >= gend);
+  short8 kr[NC];
+  if (live0) {
+    const T* krow = (j0 == t) ? kg : kcb + (int64_t)j0 * HD;
+    const T* vrow = (j0 == t) ? vg : vcb + (int64_t)j0 * HD;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) kr[c] = *reinterpret_cast<const short8*>(krow + c * 8);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      *reinterpret_cast<short8*>(vs + j0 * HD + c * 8) = *reinterpret_cast<const short8*>(vrow + c * 8);
+  }
   for (int i = tid; i < HD; i += 256) {
     qs[i] = (float)qg[i] * scale;
     kcb[(int64_t)t * HD + i] = kg[i];
     vcb[(int64_t)t * HD + i] = vg[i];
   }
   __syncthreads();
-  const int s0 = start ? start[b] : 0;
-  const int g0 = plen ? plen[b] : gend;  // masked gap [g0, gend)
   float mx = -INFINITY;
   for (int j = tid; j <= t; j += 256) {
     float s = -INFINITY;
     if (j >= s0 && (j < g0 || j >= gend)) {
-      const T* kr = (j == t) ? kg : kcb + (int64_t)j * HD;
       s = 0.f;
+      if (j == j0) {  // the prefetched row
 #pragma unroll
-      for (int c = 0; c < HD; c += 8) {
-        float kv[8];
-        load8<T>(kr + c, kv);
+        for (int c = 0; c < NC; ++c) {
+          float kv[8];
+          unpack8<T>(kr[c], kv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += qs[c + e] * kv[e];
+          for (int e = 0; e < 8; ++e) s += qs[c * 8 + e] * kv[e];
+        }
+      } else {
+        const T* krow = (j == t) ? kg : kcb + (int64_t)j * HD;
+#pragma unroll
+        for (int c = 0; c < HD; c += 8) {
+          float kv[8];
+          load8<T>(krow + c, kv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s += qs[c + e] * kv[e];
+        }
       }
     }
     sc[j] = s;
@@ -89,8 +117,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const T* __restrict__ 
   if (g < G) {
     for (int j = s0 + g; j <= t; j += G) {
       if (j >= g0 && j < gend) continue;  // gap keys: p = 0, their V rows are never read
-      const T* vr = (j == t) ? vg : vcb + (int64_t)j * HD;
-      acc += sc[j] * (float)vr[d];
+      const float vj = j < 256 ? (float)vs[j * HD + d]
+                               : (float)((j == t) ? vg : vcb + (int64_t)j * HD)[d];
+      acc += sc[j] * vj;
     }
     red[g * HD + d] = acc;
   }
@@ -107,8 +136,16 @@ template <typename T, int HD>
 void launch(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, at::Tensor& out, const int* start, const int* plen,
             int gend, int B, int H, int Tmax, int t, const int* t_dev, float scale, hipStream_t st) {
   constexpr int G = 256 / HD;
-  // score buffer for keys [0, t]; a device-side t is only bounded by the cache
-  const size_t smem = (size_t)(HD + G * HD + (t_dev ? Tmax : t + 1)) * sizeof(float);
+  // q, the reduction scratch, the staged V rows of keys 0..255, then the score buffer for keys [0, t]
+  // (a device-side t is only bounded by the cache)
+  const size_t smem = (size_t)(HD + G * HD) * sizeof(float) + (size_t)256 * HD * sizeof(T) +
+                      (size_t)(t_dev ? Tmax : t + 1) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {  // up to ~130 KB at HD 128 with a device-side position
+    (void)hipFuncSetAttribute((const void*)decode_attn_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
   hipLaunchKernelGGL((decode_attn_kernel<T, HD>), dim3(B * H), dim3(256), smem, st, (const T*)qkv.data_ptr(),
                      (T*)kc.data_ptr(), (T*)vc.data_ptr(), (T*)out.data_ptr(), start, plen, gend, H, Tmax, t, t_dev,
                      scale);
@@ -299,5 +336,57 @@ void mift_decode_tail(const at::Tensor& logits, int64_t V, at::Tensor& done, at:
   else {
     TORCH_CHECK(logits.scalar_type() == at::kHalf, "decode_tail: bf16 / fp16 logits");
     launch(fp16{});
+  }
+}
+
+namespace {
+
+// ---- prefill: the prompt's K / V rows into the caches, both in one launch ----
+// qkv [B*S, 3*H*HD] (row b*S + s), caches [B, H, Tmax, HD]: rows [0, S) of every (b, h).  One thread
+// per 16-B piece of the destination; replaces two strided torch copies per layer.
+template <typename T>
+__global__ __launch_bounds__(256) void kv_store_kernel(const T* __restrict__ qkv, T* __restrict__ kc,
+                                                       T* __restrict__ vc, int B, int S, int H, int HD, int Tmax) {
+  const int npc = HD / 8;  // pieces per row
+  const int64_t per = (int64_t)B * H * S * npc;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * per) return;
+  const bool isv = i >= per;
+  int64_t r = isv ? i - per : i;
+  const int c = (int)(r % npc);
+  r /= npc;
+  const int s = (int)(r % S);
+  r /= S;
+  const int h = (int)(r % H);
+  const int b = (int)(r / H);
+  const int64_t d = (int64_t)H * HD;
+  const T* src = qkv + ((int64_t)b * S + s) * 3 * d + (isv ? 2 : 1) * d + (int64_t)h * HD + c * 8;
+  T* dst = (isv ? vc : kc) + (((int64_t)b * H + h) * Tmax + s) * HD + c * 8;
+  *reinterpret_cast<short8*>(dst) = *reinterpret_cast<const short8*>(src);
+}
+
+}  // namespace
+
+// qkv [B*S, 3*H*HD] -> kc / vc [B, H, Tmax, HD] rows [0, S)
+void mift_kv_store(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t S) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 2, "kv_store: qkv [B*S, 3*H*HD] contiguous");
+  TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.sizes() == vc.sizes(),
+              "kv_store: caches [B,H,Tmax,HD]");
+  TORCH_CHECK(kc.scalar_type() == qkv.scalar_type() && vc.scalar_type() == qkv.scalar_type(), "kv_store: dtype");
+  const int B = kc.size(0), H = kc.size(1), Tmax = kc.size(2), HD = kc.size(3);
+  TORCH_CHECK(S >= 1 && S <= Tmax && qkv.size(0) == (int64_t)B * S && qkv.size(1) == 3LL * H * HD,
+              "kv_store: shapes");
+  TORCH_CHECK(HD % 8 == 0, "kv_store: head dim % 8");
+  const int64_t n = 2LL * B * H * S * (HD / 8);
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(kv_store_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       (const T*)qkv.data_ptr(), (T*)kc.data_ptr(), (T*)vc.data_ptr(), B, (int)S, H, HD, Tmax);
+  };
+  if (qkv.scalar_type() == at::kBFloat16) go(bf16{});
+  else {
+    TORCH_CHECK(qkv.scalar_type() == at::kHalf, "kv_store: bf16 / fp16");
+    go(fp16{});
   }
 }

@@ -104,6 +104,7 @@ at::Tensor mift_gemm_ln_fold(const at::Tensor& x, const at::Tensor& wf, const at
                              double eps, int64_t act);
 void mift_decode_tail(const at::Tensor& logits, int64_t V, at::Tensor& done, at::Tensor& ids, at::Tensor& out,
                       at::Tensor& col, at::Tensor& pos, at::Tensor& t, int64_t fill, int64_t pad, int64_t eos);
+void mift_kv_store(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t S);
 at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& vc, int64_t t, double scale,
                             const c10::optional<at::Tensor>& start, const c10::optional<at::Tensor>& plen,
                             int64_t gend, const c10::optional<at::Tensor>& t_dev);
@@ -113,6 +114,7 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
   m.def("gemm_ln", &mift_gemm_ln, "act(LN(x) w^T + bias) for M <= 64 rows (decode), LN applied in the GEMM"); \
   m.def("gemm_ln_fold", &mift_gemm_ln_fold, "act(rstd (x wf^T - mean c1) + c2): LN folded into the weights (decode)"); \
   m.def("decode_tail", &mift_decode_tail, "greedy decode step tail: argmax, pad/eos, next ids, out/col/pos/t advance"); \
+  m.def("kv_store", &mift_kv_store, "prefill: K / V rows [0, S) of qkv into the caches, one launch"); \
   m.def("decode_attn", &mift_decode_attn, "single-token attention over a KV cache; appends k/v at t (left padding: start; prompt gap: plen, gend)"); \
   m.def("lora_proj", &mift_lora_proj, "out[M,32] = alpha*drop(x)@w^T (tall-skinny MFMA)"); \
   m.def("layer_norm_fwd_proj", &mift_layer_norm_fwd_proj, "LN fwd + alpha*drop(y)@pw^T -> (y, mean, rstd, proj)"); \

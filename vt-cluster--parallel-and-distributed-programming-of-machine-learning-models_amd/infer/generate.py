@@ -67,13 +67,15 @@ def _prefill_attn(cache, li, B, S, H, hd, kv_len, fused):
 
     def attn(qkv):
         qkv3 = qkv.reshape(B, S, 3 * d)
+        if fused:
+            from ..ops import kernels as K
+            from ..ops.attention import causal_attention
+            K.kv_store(qkv.reshape(B * S, 3 * d).contiguous(), cache.k[li], cache.v[li], S)
+            return causal_attention(qkv3, B, S, H, hd, scale=scale, kv_len=kv_len)
         k = _split_heads(qkv3[..., d:2 * d], B, S, H, hd)
         v = _split_heads(qkv3[..., 2 * d:], B, S, H, hd)
         cache.k[li][:, :, :S].copy_(k)
         cache.v[li][:, :, :S].copy_(v)
-        if fused:
-            from ..ops.attention import causal_attention
-            return causal_attention(qkv3, B, S, H, hd, scale=scale, kv_len=kv_len)
         q = _split_heads(qkv3[..., :d], B, S, H, hd)
         valid = None
         if kv_len is not None:

@@ -131,6 +131,11 @@ def decode_tail(logits, V, done, ids, out, col, pos, t, fill, pad, eos):
                     -1 if eos is None else int(eos))
 
 
+def kv_store(qkv, kcache, vcache, S):
+    """Prefill: rows [0, S) of every (b, h) of the caches [B, H, Tmax, hd] from qkv [B*S, 3*H*hd]."""
+    C().kv_store(qkv, kcache, vcache, int(S))
+
+
 def decode_attn(qkv, kcache, vcache, t, scale, start=None, plen=None, gend=0):
     """o [B, H*hd] for the token at position t; writes its k/v into the caches.  Masked keys:
     ``< start[b]`` (left padding) and ``[plen[b], gend)`` (right-aligned prompts, generate.py).
