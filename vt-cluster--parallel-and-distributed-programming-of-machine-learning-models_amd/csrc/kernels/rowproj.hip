@@ -506,13 +506,34 @@ inline bool rowproj_mfma_ok(int D) {
   return !(e && atoi(e) == 1) && rowproj_width(D);
 }
 
+// waves per block at the distilgpt2 / OPT-125m widths: 12 (16 at 1024; 2 k-steps per wave).  More waves
+// per row block shorten each wave's load chain and register footprint (the LN-backward pass: ~100 VGPRs
+// on 8 waves against 174 on 4) so more waves per SIMD hide the row loads — distilgpt2 step 4.727 ->
+// 4.664 ms on 8 waves (LN-bwd + dropout-bwd + dT 17.5 -> 15 us, LN + T 11.1 -> 9.5, c_attn dT 14.3 ->
+// 10.7), 4.659 on 12 (profiles/r5/step_ab_rowproj_nw*.json).  MIFT_ROWPROJ_NW = 4 / 8 / 12 (read per
+// call): A/B.
+inline int rowproj_nw() {
+  const char* e = getenv("MIFT_ROWPROJ_NW");
+  const int v = e ? atoi(e) : 12;
+  return v == 4 || v == 8 ? v : 12;
+}
+
 // f(integral_constant NK, integral_constant NW) for a rowproj_width D
 template <typename F>
 void by_nk(int D, F&& f) {
   using std::integral_constant;
+  const int nw = rowproj_nw();
   switch (D) {
-    case 768: f(integral_constant<int, 24>{}, integral_constant<int, 4>{}); break;
-    case 1024: f(integral_constant<int, 32>{}, integral_constant<int, 4>{}); break;
+    case 768:
+      if (nw == 4) f(integral_constant<int, 24>{}, integral_constant<int, 4>{});
+      else if (nw == 12) f(integral_constant<int, 24>{}, integral_constant<int, 12>{});
+      else f(integral_constant<int, 24>{}, integral_constant<int, 8>{});
+      break;
+    case 1024:
+      if (nw == 4) f(integral_constant<int, 32>{}, integral_constant<int, 4>{});
+      else if (nw == 12) f(integral_constant<int, 32>{}, integral_constant<int, 16>{});
+      else f(integral_constant<int, 32>{}, integral_constant<int, 8>{});
+      break;
     case 2048: f(integral_constant<int, 64>{}, integral_constant<int, 8>{}); break;
     case 2560: f(integral_constant<int, 80>{}, integral_constant<int, 8>{}); break;
     default: f(integral_constant<int, 128>{}, integral_constant<int, 16>{}); break;  // 4096
@@ -523,8 +544,14 @@ void by_nk(int D, F&& f) {
 inline bool rowproj_proj_width(int K) { return rowproj_width(K) || K == 2304; }
 template <typename F>
 void by_nk_proj(int K, F&& f) {
-  if (K == 2304) f(std::integral_constant<int, 72>{}, std::integral_constant<int, 4>{});
-  else by_nk(K, f);
+  if (K == 2304) {
+    const int nw = rowproj_nw();
+    if (nw == 4) f(std::integral_constant<int, 72>{}, std::integral_constant<int, 4>{});
+    else if (nw == 12) f(std::integral_constant<int, 72>{}, std::integral_constant<int, 12>{});
+    else f(std::integral_constant<int, 72>{}, std::integral_constant<int, 8>{});
+  } else {
+    by_nk(K, f);
+  }
 }
 
 template <int LR, typename F>
