@@ -567,6 +567,29 @@ def test_gemm_epilogue_projection_matches_lora_proj(tile, rows, p):
     torch.testing.assert_close(t.float(), ref_t, atol=5e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("tile", [0, 8, 9])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_dgrad_epilogue_projection_relu_bwd(tile, dt):
+    """A dgrad GEMM with an activation-backward epilogue (ReLU-bwd on aux, OPT's fc2 dgrad) that also
+    emits the next adapter's dT = alpha·out·pwᵀ (proj_alpha = the adapter scale) == lora_proj over its
+    stored output; the GEMM output itself is unchanged by the projection."""
+    from mift.ops import kernels as K_
+    torch.manual_seed(6)
+    M, K, N, rows, s = 1024, 512, 2560, 8, 2.0
+    a = torch.randn(M, K, device="cuda").to(dt)
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).to(dt)
+    z = torch.randn(M, N, device="cuda").to(dt)
+    pw = torch.zeros(32, N, device="cuda", dtype=dt)
+    pw[:rows] = (0.05 * torch.randn(rows, N, device="cuda")).to(dt)
+    out, t = K_.gemm(a, b, act=5, aux=z, tile=tile, proj_w=pw, proj_rows=rows, proj_alpha=s)
+    out0 = K_.gemm(a, b, act=5, aux=z, tile=tile)
+    assert torch.equal(out, out0)
+    exp = K_.lora_proj(out, pw, s, 0.0, 0, rows=rows)
+    torch.testing.assert_close(t.float(), exp.float(), atol=3e-2, rtol=1e-2)
+    ref_t = s * out.float() @ pw.float().t()
+    torch.testing.assert_close(t.float(), ref_t, atol=5e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("M", [1, 7, 64])
 @pytest.mark.parametrize("N,K", [(2304, 768), (768, 3072), (50304, 768), (3072, 768)])
 def test_gemm_skinny_decode_shapes(M, N, K):

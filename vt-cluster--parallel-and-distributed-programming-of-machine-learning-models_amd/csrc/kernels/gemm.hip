@@ -2269,7 +2269,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                                      int64_t tile, const c10::optional<at::Tensor>& alpha_t,
                                      const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed,
                                      const c10::optional<at::Tensor>& proj_w, int64_t proj_rows, double proj_p,
-                                     int64_t proj_seed) {
+                                     int64_t proj_seed, double proj_alpha) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm_nt: GPU tensors required");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_nt: 2-D operands");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_nt: K must be contiguous");
@@ -2351,7 +2351,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     ep.pthr = mift_thr16(proj_p);
     ep.pseed = (uint64_t)proj_seed;
     ep.pout = proj.data_ptr();
-    ep.palpha = proj_p > 0 ? mift_inv_keep(proj_p) : 1.f;
+    ep.palpha = (float)proj_alpha * (proj_p > 0 ? mift_inv_keep(proj_p) : 1.f);
   }
   if (M == 0 || N == 0) return {c, pre, proj};
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();

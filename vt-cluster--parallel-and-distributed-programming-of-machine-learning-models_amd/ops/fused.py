@@ -91,6 +91,16 @@ def _epi_proj_kw(lo, seed, training):
     return {"proj_w": lo.A32s, "proj_rows": lo.rows, "proj_p": lo.p if training else 0.0, "proj_seed": seed}
 
 
+def _epi_dt_kw(lo):
+    """gemm kwargs that make a dgrad GEMM's epilogue emit the adapter's backward projection
+    dT = dt_alpha·out·Bᵀ of its own output (the gradient entering ``lo``'s linear) — e.g. fc2's dgrad
+    producing fc1's dz and its dT in one pass instead of a lora_proj re-reading dz (MIFT_EPI_DT=0, read
+    per call: the separate pass)."""
+    if lo is None or os.environ.get("MIFT_EPI_DT", "1") == "0":
+        return {}
+    return {"proj_w": lo.B32t, "proj_rows": lo.rows, "proj_alpha": lo.dt_alpha}
+
+
 def _claim(arena, offsets):
     """Tell the DP reducer, at forward time, that the fused backward writes these arena grads itself
     and reports them through ``_notify``.  The Functions still take the LoRA tensors as autograd
@@ -581,10 +591,13 @@ class MLP(torch.autograd.Function):
             lg2, dT2 = lo2.backward(gm, f, T2, ctx.sl2, ctx.training, dT32=dT0)
         else:
             gm = K.mask_scale(gh2, ctx.p, ctx.seed) if ctx.p > 0 else gh2
-        # dZ = (gm·W2 [+ masked LoRA ext]) ⊙ act'(z), all in the dgrad epilogue
-        dz = _dgrad(gm, fc2, lo2, dT2, ctx.sl2, ctx.training, act=_BWD[ctx.act], aux=z)
+        # dZ = (gm·W2 [+ masked LoRA ext]) ⊙ act'(z), all in the dgrad epilogue — which also emits fc1's
+        # adapter projection dT1 = s·dZ·B1 from the dZ tile it just wrote (OPT targets fc1)
+        pk = _epi_dt_kw(lo1)
+        r = _dgrad(gm, fc2, lo2, dT2, ctx.sl2, ctx.training, act=_BWD[ctx.act], aux=z, **pk)
+        dz, dT1e = r if pk else (r, None)
         if lo1 is not None:
-            lg1, dT1 = lo1.backward(dz, a, T1, ctx.sl1, ctx.training)
+            lg1, dT1 = lo1.backward(dz, a, T1, ctx.sl1, ctx.training, dT32=dT1e)
         da = _dgrad(dz, fc1, lo1, dT1, ctx.sl1, ctx.training)
         dh = _ln_bwd(ctx.hand_out, da, h2, ln_w, mean, rstd, gh2)
         return (dh.view(ctx.shp),) + (None,) * 14 + tuple(lg1) + tuple(lg2)
