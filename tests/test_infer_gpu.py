@@ -171,6 +171,14 @@ def test_graphed_decode_matches_eager(name, monkeypatch):
     monkeypatch.setenv("MIFT_GEN_GRAPH", "1")
     g_f = G.generate(m, ids_f, attention_mask=mask_f, max_new_tokens=12, eos_token_id=-1)
     assert torch.equal(e_f, g_f) and torch.equal(e_f, e.flip(0))
+    # a budget above the unroll limit: the prefill graph, then one step graph replayed per token
+    monkeypatch.setenv("MIFT_GEN_UNROLL", "4")
+    G._GRAPHS.clear()
+    s1 = G.generate(m, ids, attention_mask=mask, max_new_tokens=12, eos_token_id=-1)
+    s2 = G.generate(m, ids, attention_mask=mask, max_new_tokens=12, eos_token_id=-1)
+    assert torch.equal(e, s1) and torch.equal(e, s2)
+    monkeypatch.delenv("MIFT_GEN_UNROLL")
+    G._GRAPHS.clear()
     # early stop: identical prompts -> identical rows; EOS := the 4th generated token
     same = ids[:1].expand(4, -1).contiguous()
     msk = mask[:1].expand(4, -1).contiguous()

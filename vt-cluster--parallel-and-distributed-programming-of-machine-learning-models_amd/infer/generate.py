@@ -158,7 +158,7 @@ class _DecodeGraph:
         self.col = torch.zeros(B, 1, dtype=torch.long, device=dev)
         self.out = torch.zeros(B, max_new, dtype=torch.long, device=dev)
         self.plen = torch.zeros(B, dtype=torch.int32, device=dev) if padded else None
-        self.graph = None
+        self.graph = self.step_graph = None
 
     def prefill(self, model):
         """Prompts (static in_ids / in_lens) through the model, K/V rows [0, S0) of every layer cached,
@@ -221,7 +221,7 @@ class _DecodeGraph:
         self.lens_ev = torch.cuda.Event()
         self.lens_ev.record()
         if self.graph is not None:
-            self.graph.replay()
+            self._replay()
             return self.out
         self.call(model)  # first call of this shape: eager (first launch of every kernel module) ...
         # ... then the capture, which must rebuild every cached LoRA operand pack INSIDE the graph (each
@@ -232,18 +232,35 @@ class _DecodeGraph:
         toks = self.out.clone()
         from ..ops.fused import invalidate_packs
         invalidate_packs(model)
-        g = torch.cuda.CUDAGraph()
+        # up to MIFT_GEN_UNROLL (64) steps are unrolled into the one graph; longer budgets capture the
+        # prefill and ONE step and replay the step graph per token (graph size stays ~35 nodes per step)
+        unroll = self.max_new - 1 <= int(os.environ.get("MIFT_GEN_UNROLL", "64"))
         was = gc.isenabled()
         gc.collect()
         gc.disable()  # no finalizers of device objects inside the capture (train/graph.py)
         try:
-            with torch.cuda.graph(g):
-                self.call(model)
+            if unroll:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.call(model)
+                self.graph, self.step_graph = g, None
+            else:
+                g, gs = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.prefill(model)
+                with torch.cuda.graph(gs, pool=g.pool()):
+                    self.step(model)
+                self.graph, self.step_graph = g, gs
         finally:
             if was:
                 gc.enable()
-        self.graph = g
         return toks
+
+    def _replay(self):
+        self.graph.replay()
+        if self.step_graph is not None:
+            for _ in range(self.max_new - 1):
+                self.step_graph.replay()
 
 
 _GRAPHS = {}
