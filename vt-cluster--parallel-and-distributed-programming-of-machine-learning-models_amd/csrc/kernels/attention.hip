@@ -1358,7 +1358,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 2 : 1) void attn_fwd2_kernel(co
                                                             float* __restrict__ lse, const int* __restrict__ kv_len,
                                                             int B, int S, int H, float scale, uint64_t seed,
                                                             const int64_t* __restrict__ sstep, uint32_t thr,
-                                                            float inv_keep, uint16_t* __restrict__ dmask) {
+                                                            float inv_keep, uint16_t* __restrict__ dmask, int xcd) {
   seed = mift_seed(seed, sstep);
   using G = Geo2<HD>;
   constexpr int NT = NW * 64;
@@ -1370,7 +1370,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 2 : 1) void attn_fwd2_kernel(co
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, qi = lane & 31;
   const int nqt = (S + BQB - 1) / BQB;
-  const int bid = attn_block_id(0);
+  const int bid = attn_block_id(xcd);
   const int qt = nqt - 1 - (bid % nqt);  // heavy (late) query tiles first
   const int bh = bid / nqt;
   const int b = bh / H, h = bh % H;
@@ -1567,6 +1567,9 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 2 : 1) void attn_fwd2_kernel(co
 // distilgpt2 33.4 vs 27.2 us, OPT-2.7B 65.5 vs 62.1 us, OPT-6.7B 192 vs 159 us; profiles/r3/
 // bench_attn_v1_v2.txt) — register pressure (hd 128: 343 VGPR -> one wave per SIMD) and two
 // barriers per 64-key tile with only 4-8 waves per CU; kept (tested) for the record.
+// v2 forward (32x32x16, opt-in MIFT_ATTN_FWD=2): with the XCD-aware tile mapping too it stays behind v1
+// (OPT-2.7B 57.0 vs 49.6 us, OPT-6.7B 168 vs 117, distilgpt2 31.8 vs 23.1;
+// profiles/r5/bench_attn_fwd_v1_v2_xcd.json)
 bool attn_fwd_v2(int hd, bool seq) {
   (void)seq;
   const char* e = getenv("MIFT_ATTN_FWD");
@@ -1596,7 +1599,8 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
     const int nqt = (S + 32 * NW - 1) / (32 * NW);
     hipLaunchKernelGGL((attn_fwd2_kernel<T, HD, NW>), dim3(B * H * nqt), dim3(NW * 64), G2::K_BYTES + G2::V_BYTES,
                        st, (const T*)qkv.data_ptr(), (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale,
-                       seed, mift_seed_step(), thr, inv_keep, (seq && thr != 0) ? dmask : nullptr);
+                       seed, mift_seed_step(), thr, inv_keep, (seq && thr != 0) ? dmask : nullptr,
+                       seq ? 0 : attn_xcd_env());
     return;
   }
   // transposed-output P·V (read per call: A/B): on for the whole-sequence kernel (distilgpt2 fwd 23.3 ->
