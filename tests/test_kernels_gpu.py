@@ -306,7 +306,7 @@ def test_flash_attention_kv_len():
 
 
 @pytest.mark.parametrize("p", [0.0, 0.05])
-@pytest.mark.parametrize("K", [768, 2304, 3072, 2560, 4096])
+@pytest.mark.parametrize("K", [768, 2304, 3072, 2560, 4096, 7680])
 @pytest.mark.parametrize("M,nz", [(1000, 8), (1000, 24), (24576, 8)])
 def test_lora_proj_and_wgrad(p, K, M, nz):
     """lora_proj for every block geometry (16- and 32-row blocks, one or two 16-column tiles:

@@ -541,6 +541,8 @@ void by_nk(int D, F&& f) {
 }
 
 // the plain projection (MODE 2): the rowproj widths plus K = 2304 (distilgpt2's c_attn dT)
+// (K = 7680, OPT-2.7B's fused q/k/v dT, on 16 waves x 15 k-steps measured 40.7 / 131 us against
+// lora_proj's own kernel's 39.6 / 106 us at 6144 / 24576 rows: profiles/r5/bench_rowproj_opt_k7680.json)
 inline bool rowproj_proj_width(int K) { return rowproj_width(K) || K == 2304; }
 template <typename F>
 void by_nk_proj(int K, F&& f) {
