@@ -78,3 +78,20 @@ def test_generate_rejects_right_padding():
     left = torch.tensor([[0, 0, 1, 1, 1, 1], [1, 1, 1, 1, 1, 1]])
     out = generate(m, ids, attention_mask=left, max_new_tokens=3, eos_token_id=-1)
     assert out.shape == (2, 9) and torch.equal(out[:, :6], ids)
+
+
+def test_arena_version_follows_bumps_and_new_arenas():
+    """The graphed generate() key reads the arena through a remembered module (no module walk per
+    call): it follows version bumps and a NEW arena bound to the same model, and None without one."""
+    from mift import lora as L
+    from mift.infer import generate as G
+    from mift.models import build_causal_lm
+    m = build_causal_lm("opt-tiny", dtype=torch.float32, seed=0)
+    assert G._arena_version(m) is None
+    L.inject(m, L.LoraConfig(r=8, lora_alpha=16, target_modules=["q_proj", "v_proj"]))
+    a = L.LoraArena(m)
+    assert G._arena_version(m) == (id(a), 0)
+    a.bump()
+    assert G._arena_version(m) == (id(a), 1)
+    b = L.LoraArena(m)
+    assert G._arena_version(m) == (id(b), 0)
