@@ -590,6 +590,37 @@ def test_dgrad_epilogue_projection_relu_bwd(tile, dt):
     torch.testing.assert_close(t.float(), ref_t, atol=5e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("tile", [0, 7, 8, 9])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_relu_sign_bits_roundtrip(tile, dt):
+    """ReLU sign bits: the forward epilogue's bits are the packed (stored output > 0) mask (skinny-sized M
+    included: the bits keep such GEMMs on the tiled path), and the ReLU backward reading them is
+    bit-identical to the one reading the 16-bit output as aux — with the masked LoRA extension and the
+    dT projection epilogue on top (OPT's fc2 dgrad)."""
+    from mift.ops import kernels as K_
+    torch.manual_seed(7)
+    for M, K, N in ((1024, 512, 2560), (40, 256, 768)):
+        a = torch.randn(M, K, device="cuda").to(dt)
+        b = (torch.randn(N, K, device="cuda") / K ** 0.5).to(dt)
+        bias = (0.1 * torch.randn(N, device="cuda")).to(dt)
+        bits = torch.full((M, N // 8), 0xA5, dtype=torch.uint8, device="cuda")
+        f = K_.gemm(a, b, bias, act=2, sbits=bits, tile=tile)
+        assert torch.equal(f, K_.gemm(a, b, bias, act=2, tile=tile))
+        w8 = (1 << torch.arange(8, device="cuda", dtype=torch.int32))
+        exp = ((f > 0).view(M, N // 8, 8).to(torch.int32) * w8).sum(-1).to(torch.uint8)
+        assert torch.equal(bits, exp)
+        g = torch.randn(M, K, device="cuda").to(dt)
+        bt = (torch.randn(N, K, device="cuda") / K ** 0.5).to(dt)
+        a2 = (0.1 * torch.randn(M, 32, device="cuda")).to(dt)
+        b2 = (0.1 * torch.randn(N, 32, device="cuda")).to(dt)
+        pw = torch.zeros(32, N, device="cuda", dtype=dt)
+        pw[:8] = (0.05 * torch.randn(8, N, device="cuda")).to(dt)
+        kw = dict(a2=a2, b2=b2, ext_p=0.05, ext_seed=11, act=5, tile=tile, proj_w=pw, proj_rows=8, proj_alpha=2.0)
+        o1, t1 = K_.gemm(g, bt, aux=f, **kw)
+        o2, t2 = K_.gemm(g, bt, sbits=bits, **kw)
+        assert torch.equal(o1, o2) and torch.equal(t1, t2)
+
+
 @pytest.mark.parametrize("M", [1, 7, 64])
 @pytest.mark.parametrize("N,K", [(2304, 768), (768, 3072), (50304, 768), (3072, 768)])
 def test_gemm_skinny_decode_shapes(M, N, K):

@@ -58,6 +58,9 @@ def main():
                 r["+bias+ext+relu"] = t(bias=bias, a2=a2, b2=b2, act=2)
                 r["+bias+ext+relu+proj"] = t(bias=bias, a2=a2, b2=b2, act=2, proj_w=pw, proj_rows=16,
                                              proj_p=0.05, proj_seed=5)
+                bits = torch.empty(M, N // 8, dtype=torch.uint8, device=dev)
+                r["+bias+ext+relu+proj+bits"] = t(bias=bias, a2=a2, b2=b2, act=2, proj_w=pw, proj_rows=16,
+                                                  proj_p=0.05, proj_seed=5, sbits=bits)
             if name in ("out.fwd", "fc2.fwd"):
                 r["+bias+ext+drop+res"] = t(bias=bias, a2=a2, b2=b2, residual=res, dropout_p=0.1, seed=3)
         else:
@@ -66,6 +69,11 @@ def main():
                 r["+ext_masked+relu_bwd"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3, act=5, aux=aux)
                 r["+ext_masked+relu_bwd+proj"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3, act=5, aux=aux,
                                                    proj_w=pw, proj_rows=16, proj_alpha=2.0)
+                bits = torch.empty(M, N // 8, dtype=torch.uint8, device=dev)
+                K.gemm(A, w, act=2, sbits=bits, tile=8)  # sign bits of some ReLU output
+                r["+ext_masked+relu_bwd_bits"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3, act=5, sbits=bits)
+                r["+ext_masked+relu_bwd_bits+proj"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3, act=5, sbits=bits,
+                                                        proj_w=pw, proj_rows=16, proj_alpha=2.0)
         r["plain_pf"] = round(r["tflop"] / r["plain"] * 1e3, 3)
         print(json.dumps(r), flush=True)
         out.append(r)

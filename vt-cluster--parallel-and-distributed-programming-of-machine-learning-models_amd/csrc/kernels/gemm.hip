@@ -126,6 +126,9 @@ struct EpiArgs {
   float* pws;
   void* pout;
   float palpha;
+  // ReLU sign bits [M][N/8] (bit e of byte (row, col/8) = stored output (row, col + e) > 0): written by an
+  // ACT_RELU epilogue, read by ACT_RELU_BWD in place of the 16-bit aux (1/16 of its bytes)
+  uint8_t* sbits;
 };
 
 // Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
@@ -611,7 +614,11 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         if (full) store8<T>(reinterpret_cast<T*>(ep.preact) + off, z);
         else for (int e = 0; e < N - gc; ++e) reinterpret_cast<T*>(ep.preact)[off + e] = (T)z[e];
       }
-      if (ep.act != ACT_NONE) {
+      if (ep.act == ACT_RELU_BWD && ep.aux == nullptr && ep.sbits != nullptr) {
+        const uint32_t sb = ep.sbits[(size_t)gr * (N >> 3) + (gc >> 3)];
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = (sb >> e) & 1u ? z[e] : 0.f;
+      } else if (ep.act != ACT_NONE) {
         float ax[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (ep.aux != nullptr) {
           if (full && have_aux) unpack8<T>(auxv, ax);
@@ -661,6 +668,12 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         for (int e = 0; e < 8; ++e) { T t = (T)z[e]; short h; __builtin_memcpy(&h, &t, 2); o[e] = h; }
         CT::write8(Cs, row, c8, o);
       }
+      if (ep.sbits != nullptr && ep.act == ACT_RELU) {  // N % 8 == 0 (host): every chunk is full
+        uint32_t sb = 0;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) sb |= ((float)(T)z[e] > 0.f ? 1u : 0u) << e;
+        ep.sbits[(size_t)gr * (N >> 3) + (gc >> 3)] = (uint8_t)sb;
+      }
       if (ep.lm.dbg & 1) return;  // diagnostics: MIFT_LM_DBG bit 0 skips the C store
       if (full) store8<T>(C + off, z);
       else for (int e = 0; e < N - gc; ++e) C[off + e] = (T)z[e];
@@ -676,6 +689,20 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       const bool hz = (uint64_t)M * N < (1ull << 33);
       const int PW = ep.prow <= 16 ? 16 : 32;
       float* slab = ep.pws + (size_t)(n0 / BN) * M * PW;
+      // the pw fragments depend on (s, j, lane) only: loaded once for all of the wave's row stripes
+      // (they were re-requested per stripe, one dependent L2 round trip each)
+      short8 pwv[BN / 32][2];
+  #pragma unroll
+      for (int s = 0; s < BN / 32; ++s) {
+        const int gc = n0 + s * 32 + g * 8;
+  #pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int wr = j * 16 + fr;
+          pwv[s][j] = (j * 16 < ep.prow && wr < ep.prow && gc < N)
+                          ? *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.pw) + (size_t)wr * N + gc)
+                          : short8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+      }
       for (int rt = wave; rt < BM / 16; rt += NW) {
         const int row = rt * 16 + fr, gr = m0 + row;
         float4_ pacc[2] = {float4_{0.f, 0.f, 0.f, 0.f}, float4_{0.f, 0.f, 0.f, 0.f}};
@@ -697,12 +724,8 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   #pragma unroll
           for (int j = 0; j < 2; ++j) {
             if (j * 16 >= ep.prow) break;  // uniform: rows >= prow of pw are zero
-            const int wr = j * 16 + fr;
-            const short8 bv = (wr < ep.prow && gc < N)
-                                  ? *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.pw) + (size_t)wr * N + gc)
-                                  : short8{0, 0, 0, 0, 0, 0, 0, 0};
             frag_t<T> bf;
-            __builtin_memcpy(&bf, &bv, 16);
+            __builtin_memcpy(&bf, &pwv[s][j], 16);
             pacc[j] = mfma16<T>(bf, af, pacc[j]);  // lane: out[row fr][16j + 4g .. +3]
           }
         }
@@ -1873,7 +1896,7 @@ bool skinny_ok(int M, int N, int K, const EpiArgs& ep) {
   static const int env = [] { const char* e = getenv("MIFT_GEMM_SKINNY"); return e ? atoi(e) : 1; }();
   if (!env || M > 64 || N % 16 != 0) return false;
   if (N > 4096 ? (K > 1024 || N % 64 != 0 || env < 2) : (K > 4096 || (K > 1024 && (K / 32) % ((K + 1023) / 1024)))) return false;
-  if (ep.thr != 0 || ep.ext_thr != 0 || ep.aux != nullptr || ep.lm.dbg != 0) return false;
+  if (ep.thr != 0 || ep.ext_thr != 0 || ep.aux != nullptr || ep.sbits != nullptr || ep.lm.dbg != 0) return false;
   if (ep.act != ACT_NONE && ep.act != ACT_GELU_TANH && ep.act != ACT_RELU && ep.act != ACT_GELU_ERF) return false;
   if (ep.pw != nullptr && ep.pthr != 0) return false;
   return true;
@@ -2269,7 +2292,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                                      int64_t tile, const c10::optional<at::Tensor>& alpha_t,
                                      const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed,
                                      const c10::optional<at::Tensor>& proj_w, int64_t proj_rows, double proj_p,
-                                     int64_t proj_seed, double proj_alpha) {
+                                     int64_t proj_seed, double proj_alpha, const c10::optional<at::Tensor>& sbits) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm_nt: GPU tensors required");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_nt: 2-D operands");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_nt: K must be contiguous");
@@ -2352,6 +2375,14 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     ep.pseed = (uint64_t)proj_seed;
     ep.pout = proj.data_ptr();
     ep.palpha = (float)proj_alpha * (proj_p > 0 ? mift_inv_keep(proj_p) : 1.f);
+  }
+  ep.sbits = nullptr;
+  if (sbits) {  // ReLU sign bits: written (act = relu) or read in place of aux (act = relu backward)
+    TORCH_CHECK((act == ACT_RELU || (act == ACT_RELU_BWD && !aux)) && N % 8 == 0 && sbits->is_cuda() &&
+                    sbits->scalar_type() == at::kByte && sbits->is_contiguous() && sbits->size(0) == M &&
+                    sbits->size(1) == N / 8,
+                "gemm_nt: sbits must be uint8 [M, N/8] with act relu / relu-bwd (no aux), N % 8 == 0");
+    ep.sbits = sbits->data_ptr<uint8_t>();
   }
   if (M == 0 || N == 0) return {c, pre, proj};
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();

@@ -24,7 +24,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
                                      int64_t tile, const c10::optional<at::Tensor>& alpha_t,
                                      const c10::optional<at::Tensor>& pre_add, double ext_p, int64_t ext_seed,
                                      const c10::optional<at::Tensor>& proj_w, int64_t proj_rows, double proj_p,
-                                     int64_t proj_seed, double proj_alpha);
+                                     int64_t proj_seed, double proj_alpha, const c10::optional<at::Tensor>& sbits);
 
 // ---- K2/K7 fused LM head + cross-entropy (kernels/gemm.hip, EPI 1/2)
 std::vector<at::Tensor> mift_lmhead_fwd(const at::Tensor& a, const at::Tensor& w, const at::Tensor& labels, int64_t V,
@@ -134,7 +134,8 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
         pybind11::arg("seed"), pybind11::arg("want_preact"), pybind11::arg("alpha"), pybind11::arg("out"), \
         pybind11::arg("tile"), pybind11::arg("alpha_t"), pybind11::arg("pre_add"), pybind11::arg("ext_p"), \
         pybind11::arg("ext_seed"), pybind11::arg("proj_w") = pybind11::none(), pybind11::arg("proj_rows") = 32, \
-        pybind11::arg("proj_p") = 0.0, pybind11::arg("proj_seed") = 0, pybind11::arg("proj_alpha") = 1.0); \
+        pybind11::arg("proj_p") = 0.0, pybind11::arg("proj_seed") = 0, pybind11::arg("proj_alpha") = 1.0, \
+        pybind11::arg("sbits") = pybind11::none()); \
   m.def("lmhead_fwd", &mift_lmhead_fwd, "fused LM head + CE fwd -> (E, stats, lse, loss, zlab[, total])"); \
   m.def("lmhead_dgrad", &mift_lmhead_dgrad, "fused LM head + CE dgrad -> dX (no dlogits)"); \
   m.def("grad_stats", &mift_grad_stats, "sum(g^2), nonfinite count -> stats[2]"); \

@@ -560,9 +560,13 @@ class MLP(torch.autograd.Function):
         # tile partials + one ordered reduction) instead of a lora_proj pass re-reading f
         pk = _epi_proj_kw(lo2, seed_l2, training)
         if act == 2:  # ReLU: relu'(z) = [f > 0], so f doubles as the backward's aux (no pre-activation store)
-            r = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, **pk)
+            # ... or, 16x fewer bytes for the dgrad epilogue to read, the sign bits of f (MIFT_RELU_BITS=0: f)
+            N1 = fc1.w_nk().shape[0]
+            bits = (torch.empty(h2.shape[0], N1 // 8, dtype=torch.uint8, device=h2.device)
+                    if N1 % 8 == 0 and os.environ.get("MIFT_RELU_BITS", "1") != "0" else None)
+            r = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, sbits=bits, **pk)
             f, T2 = r if pk else (r, None)
-            z = f
+            z = f if bits is None else bits
         else:
             r = K.gemm(a, fc1.w_nk(), fc1.bias, T1, lo1.B32 if lo1 else None, act=act, want_preact=True, **pk)
             f, z, T2 = r if pk else r + (None,)
@@ -594,7 +598,10 @@ class MLP(torch.autograd.Function):
         # dZ = (gm·W2 [+ masked LoRA ext]) ⊙ act'(z), all in the dgrad epilogue — which also emits fc1's
         # adapter projection dT1 = s·dZ·B1 from the dZ tile it just wrote (OPT targets fc1)
         pk = _epi_dt_kw(lo1)
-        r = _dgrad(gm, fc2, lo2, dT2, ctx.sl2, ctx.training, act=_BWD[ctx.act], aux=z, **pk)
+        if z.dtype == torch.uint8:  # ReLU sign bits of f (forward)
+            r = _dgrad(gm, fc2, lo2, dT2, ctx.sl2, ctx.training, act=_BWD[ctx.act], sbits=z, **pk)
+        else:
+            r = _dgrad(gm, fc2, lo2, dT2, ctx.sl2, ctx.training, act=_BWD[ctx.act], aux=z, **pk)
         dz, dT1e = r if pk else (r, None)
         if lo1 is not None:
             lg1, dT1 = lo1.backward(dz, a, T1, ctx.sl1, ctx.training, dT32=dT1e)

@@ -13,17 +13,20 @@ ACT_BWD = {0: 0, 1: 4, 2: 5, 3: 6}
 
 def gemm(a, b, bias=None, a2=None, b2=None, act=0, aux=None, residual=None, dropout_p=0.0, seed=0,
          want_preact=False, alpha=1.0, out=None, tile=0, alpha_t=None, pre_add=None, ext_p=0.0, ext_seed=0,
-         proj_w=None, proj_rows=32, proj_p=0.0, proj_seed=0, proj_alpha=1.0):
+         proj_w=None, proj_rows=32, proj_p=0.0, proj_seed=0, proj_alpha=1.0, sbits=None):
     """out = epi(a @ b.T [+ a2 @ b2.T]); see csrc/kernels/gemm.hip.
 
     ``ext_p > 0`` keeps the a2·b2ᵀ K-extension separate and adds it under the
     dropout mask (ext_seed, ext_p) — the LoRA input-dropout backward.
     ``proj_w`` ([32, N], first ``proj_rows`` rows non-zero): also return
     T = proj_alpha · dropout(out; proj_p, proj_seed) @ proj_w.T [M, 32] computed in the epilogue
-    (= lora_proj(out, proj_w, proj_alpha, proj_p, proj_seed) without re-reading out)."""
+    (= lora_proj(out, proj_w, proj_alpha, proj_p, proj_seed) without re-reading out).
+    ``sbits`` (uint8 [M, N/8]): with ``act`` = ReLU the epilogue writes the sign bits of the stored
+    output into it; with the ReLU backward (``act`` = 5, no ``aux``) it reads them as the mask."""
     y, pre, t = C().gemm_nt(a, b, bias, a2, b2, int(act), aux, residual, float(dropout_p), int(seed),
                             bool(want_preact), float(alpha), out, int(tile), alpha_t, pre_add, float(ext_p),
-                            int(ext_seed), proj_w, int(proj_rows), float(proj_p), int(proj_seed), float(proj_alpha))
+                            int(ext_seed), proj_w, int(proj_rows), float(proj_p), int(proj_seed), float(proj_alpha),
+                            sbits)
     res = (y, pre) if want_preact else (y,)
     if proj_w is not None:
         res = res + (t,)
