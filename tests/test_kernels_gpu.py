@@ -605,7 +605,8 @@ def test_relu_sign_bits_roundtrip(tile, dt):
         bias = (0.1 * torch.randn(N, device="cuda")).to(dt)
         bits = torch.full((M, N // 8), 0xA5, dtype=torch.uint8, device="cuda")
         f = K_.gemm(a, b, bias, act=2, sbits=bits, tile=tile)
-        assert torch.equal(f, K_.gemm(a, b, bias, act=2, tile=tile))
+        # auto at M <= 64 without bits is the skinny kernel (another accumulation order): the tiled 64x64
+        assert torch.equal(f, K_.gemm(a, b, bias, act=2, tile=4 if (tile == 0 and M <= 64) else tile))
         w8 = (1 << torch.arange(8, device="cuda", dtype=torch.int32))
         exp = ((f > 0).view(M, N // 8, 8).to(torch.int32) * w8).sum(-1).to(torch.uint8)
         assert torch.equal(bits, exp)
