@@ -63,6 +63,9 @@ def main():
                                                   proj_p=0.05, proj_seed=5, sbits=bits)
             if name in ("out.fwd", "fc2.fwd"):
                 r["+bias+ext+drop+res"] = t(bias=bias, a2=a2, b2=b2, residual=res, dropout_p=0.1, seed=3)
+                os.environ["MIFT_EPI_PFG"] = "0"  # operands per chunk (the old rolled loop)
+                r["+bias+ext+drop+res_pfg0"] = t(bias=bias, a2=a2, b2=b2, residual=res, dropout_p=0.1, seed=3)
+                os.environ.pop("MIFT_EPI_PFG")
         else:
             r["+ext_masked"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3)
             if name == "fc2.dgrad":
@@ -74,6 +77,13 @@ def main():
                 r["+ext_masked+relu_bwd_bits"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3, act=5, sbits=bits)
                 r["+ext_masked+relu_bwd_bits+proj"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3, act=5, sbits=bits,
                                                         proj_w=pw, proj_rows=16, proj_alpha=2.0)
+        if name == "fc2.dgrad":  # operands per chunk (the old rolled loop)
+            os.environ["MIFT_EPI_PFG"] = "0"
+            r["+ext_masked+relu_bwd_bits+proj_pfg0"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3, act=5, sbits=bits,
+                                                         proj_w=pw, proj_rows=16, proj_alpha=2.0)
+            r["+ext_masked+relu_bwd+proj_pfg0"] = t(a2=a2, b2=b2, ext_p=0.05, ext_seed=3, act=5, aux=aux,
+                                                    proj_w=pw, proj_rows=16, proj_alpha=2.0)
+            os.environ.pop("MIFT_EPI_PFG")
         r["plain_pf"] = round(r["tflop"] / r["plain"] * 1e3, 3)
         print(json.dumps(r), flush=True)
         out.append(r)

@@ -129,6 +129,7 @@ struct EpiArgs {
   // ReLU sign bits [M][N/8] (bit e of byte (row, col/8) = stored output (row, col + e) > 0): written by an
   // ACT_RELU epilogue, read by ACT_RELU_BWD in place of the 16-bit aux (1/16 of its bytes)
   uint8_t* sbits;
+  int pfg;        // 256x256 epilogue: operands requested per group of 4 chunks (MIFT_EPI_PFG, default 1)
 };
 
 // Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
@@ -594,7 +595,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       }
     };
     // one 8-column chunk: (aux, res) come prefetched when have_aux / have_res
-    auto chunk = [&](int it, bool have_aux, short8 auxv, bool have_res, short8 resv) {
+    auto chunk = [&](int it, bool have_aux, short8 auxv, bool have_res, short8 resv, int sbp) {
       const int v = tid + it * NT;
       const int row = v / VPR, c8 = (v % VPR) * 8;
       const int gr = m0 + row, gc = n0 + c8;
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         else for (int e = 0; e < N - gc; ++e) reinterpret_cast<T*>(ep.preact)[off + e] = (T)z[e];
       }
       if (ep.act == ACT_RELU_BWD && ep.aux == nullptr && ep.sbits != nullptr) {
-        const uint32_t sb = ep.sbits[(size_t)gr * (N >> 3) + (gc >> 3)];
+        const uint32_t sb = sbp >= 0 ? (uint32_t)sbp : ep.sbits[(size_t)gr * (N >> 3) + (gc >> 3)];
   #pragma unroll
         for (int e = 0; e < 8; ++e) z[e] = (sb >> e) & 1u ? z[e] : 0.f;
       } else if (ep.act != ACT_NONE) {
@@ -683,7 +684,11 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     // stripe per wave; the LoRA-input dropout mask of element (row, col) is the consumer's
     // (index row·N + col, as lora_proj / lora_wgrad / the dgrad K-extension regenerate it).
     auto proj_phase = [&]() {
-      __syncthreads();  // every chunk's output is in the C tile
+      // every chunk's output is in the C tile: an LDS-only barrier (phase 2's global stores may stay in
+      // flight; measured neutral against __syncthreads() at OPT's shapes, profiles/r5/bench_opt_epilogue_pfg.json)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       const int fr = lane & 15, g = lane >> 4;
       const uint32_t hm0 = mift_hmix(ep.pseed, 0);
       const bool hz = (uint64_t)M * N < (1ull << 33);
@@ -738,16 +743,39 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     };
     if constexpr (PF_OK) {
       if (!ep.prefetch) {
-        for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{});
+        for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{}, -1);
       } else {
         short8 aux_r[ITER], res_r[ITER];
         if (pf_aux) prefetch(ep.aux, aux_r);
         if (pf_res) prefetch(ep.residual, res_r);
   #pragma unroll
-        for (int it = 0; it < ITER; ++it) chunk(it, pf_aux, aux_r[it], pf_res, res_r[it]);
+        for (int it = 0; it < ITER; ++it) chunk(it, pf_aux, aux_r[it], pf_res, res_r[it], -1);
       }
     } else {
-      for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{});
+      // 256x256 (16 chunks per thread, one block per CU: no second block hides a chunk's operand round
+      // trip, ~1 us from HBM, paid 16 times per tile in the rolled loop — OPT's residual-dropout
+      // epilogues cost +51..62 us per GEMM at micro-batch 48): groups of 4 chunks request their aux /
+      // residual / sign-bit operands together, one round trip per group.  MIFT_EPI_PFG=0: per chunk (A/B)
+      constexpr int G = 4;
+      static_assert(ITER % G == 0, "chunk groups");
+      const bool g_aux = ep.pfg && ep.aux != nullptr && ep.act != ACT_NONE && N >= 8;
+      const bool g_res = ep.pfg && ep.residual != nullptr && N >= 8;
+      const bool g_sb = ep.pfg && ep.sbits != nullptr && ep.act == ACT_RELU_BWD && ep.aux == nullptr;
+      for (int g0 = 0; g0 < ITER; g0 += G) {
+        short8 av[G], rv[G];
+        int bv[G];
+  #pragma unroll
+        for (int k = 0; k < G; ++k) {
+          const int v = tid + (g0 + k) * NT;
+          const int gr = min(m0 + v / VPR, M - 1), gc = min(n0 + (v % VPR) * 8, N - 8);
+          const size_t o = (size_t)gr * ldc + gc;
+          av[k] = g_aux ? *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.aux) + o) : short8{};
+          rv[k] = g_res ? *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(ep.residual) + o) : short8{};
+          bv[k] = g_sb ? (int)ep.sbits[(size_t)gr * (N >> 3) + (gc >> 3)] : -1;
+        }
+  #pragma unroll
+        for (int k = 0; k < G; ++k) chunk(g0 + k, g_aux, av[k], g_res, rv[k], bv[k]);
+      }
     }
     if (ep.pws != nullptr) proj_phase();
   };
@@ -2354,6 +2382,10 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     ep.prefetch = e ? atoi(e) : 0;
   }
   ep.group_m = gemm_group_m(N);
+  {
+    const char* e = getenv("MIFT_EPI_PFG");  // read per call (A/B)
+    ep.pfg = e ? atoi(e) : 1;
+  }
   if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);  // diagnostics (bit 0: no C store)
   ep.pre_add = nullptr;
   if (pre_add) {
