@@ -1426,26 +1426,38 @@ int gemm_group_m(int N) {
 }
 
 // out[m, 0:32] = alpha · Σ_t slab[t][m][0:PW] (columns >= PW zero): the per-column-tile partials of
-// the epilogue projection, summed in tile order (8 outputs per thread)
+// the epilogue projection, summed in tile order.  4 outputs per thread (every thread of a 16-wide slab
+// loads: the 8-per-thread form idled half of them), 8 tiles' loads requested before their adds (the
+// rolled loop paid one dependent round trip per tile: 27.5 us for OPT fc1's 63 MB of slabs at mb 48)
 template <typename T>
 __global__ __launch_bounds__(256) void proj_reduce_kernel(const float* __restrict__ slab, int ntn, int M, int PW,
                                                           float alpha, T* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (row, 8-column group)
-  if (i >= (int64_t)M * 4) return;
-  const int m = (int)(i >> 2), c8 = (int)(i & 3) * 8;
-  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (c8 < PW) {
-    for (int t = 0; t < ntn; ++t) {
-      const float* p = slab + ((size_t)t * M + m) * PW + c8;
-      const float4 a = *reinterpret_cast<const float4*>(p);
-      const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (row, 4-column group)
+  if (i >= (int64_t)M * 8) return;
+  const int m = (int)(i >> 3), c4 = (int)(i & 7) * 4;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c4 < PW) {
+    const float* p = slab + (size_t)m * PW + c4;
+    const size_t ts = (size_t)M * PW;
+    int t = 0;
+    for (; t + 8 <= ntn; t += 8) {
+      float4 a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = *reinterpret_cast<const float4*>(p + (size_t)(t + u) * ts);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[0] += a[u].x; v[1] += a[u].y; v[2] += a[u].z; v[3] += a[u].w;
+      }
+    }
+    for (; t < ntn; ++t) {
+      const float4 a = *reinterpret_cast<const float4*>(p + (size_t)t * ts);
       v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
     }
   }
+  float o[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] *= alpha;
-  store8<T>(out + (size_t)m * 32 + c8, v);
+  for (int e = 0; e < 4; ++e) o[e] = v[e] * alpha;
+  store4<T>(out + (size_t)m * 32 + c4, o);
 }
 
 template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, int KB = 64>
@@ -1513,7 +1525,7 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const 
                        (int)b.stride(0), (int)c.stride(0), epx, sk);
   }
   if (ep.pw != nullptr)
-    hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 8 + 255) / 256)), dim3(256), 0, st,
                        (const float*)epx.pws, ntn, M, PW, ep.palpha, (T*)ep.pout);
 }
 
@@ -1915,7 +1927,7 @@ void launch_skinny(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
                        (const T*)nullptr, 0.f, ksplit, kws, kflags, pfe, (const float*)nullptr, (const float*)nullptr);
   }
   if (ep.pw != nullptr)
-    hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 4 + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(proj_reduce_kernel<T>, dim3((unsigned)(((int64_t)M * 8 + 255) / 256)), dim3(256), 0, st,
                        (const float*)epx.pws, nb, M, PW, ep.palpha, (T*)ep.pout);
 }
 
