@@ -584,8 +584,9 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     // loop stays rolled: unrolling it with the generic activation switch cost the 256x256 ReLU
     // epilogues 20 % (OPT fc1 fwd 1395 -> 1121 us, fc2 dgrad 1594 -> 1321 us at M = 24576).
     constexpr bool PF_OK = ITER <= 8;
-    const bool pf_aux = PF_OK && ep.prefetch && ep.aux != nullptr && ep.act != ACT_NONE && N >= 8;
-    const bool pf_res = PF_OK && ep.prefetch && ep.residual != nullptr && N >= 8;
+    // MIFT_EPI_PREFETCH: 1 = aux and residual, 2 = residual only
+    const bool pf_aux = PF_OK && ep.prefetch == 1 && ep.aux != nullptr && ep.act != ACT_NONE && N >= 8;
+    const bool pf_res = PF_OK && ep.prefetch != 0 && ep.residual != nullptr && N >= 8;
     auto prefetch = [&](const void* src, short8* dst) {
   #pragma unroll
       for (int it = 0; it < ITER; ++it) {
