@@ -57,6 +57,12 @@ OPT_SHAPES = [  # OPT-2.7B, 8x512 tokens per micro-batch (every distinct GEMM of
 ]
 
 
+# the eight distinct GEMMs of an OPT-2.7B layer (forward + dgrad), N x K at M = micro-batch x 512
+OPT_LAYER = [("opt.qkv.fwd", 7680, 2560), ("opt.out.fwd", 2560, 2560), ("opt.fc1.fwd", 10240, 2560),
+             ("opt.fc2.fwd", 2560, 10240), ("opt.qkv.dgrad", 2560, 7680), ("opt.out.dgrad", 2560, 2560),
+             ("opt.fc1.dgrad", 2560, 10240), ("opt.fc2.dgrad", 10240, 2560)]
+
+
 def bench_gemm(results, shapes=None, dtype=torch.bfloat16):
     import mift._C as C
     for name, M, N, K in shapes or GEMM_SHAPES:
@@ -187,6 +193,9 @@ def main():
     for k in a.only.split(","):
         {"gemm": bench_gemm, "ln": bench_ln, "dgpt": bench_dgpt, "epi": bench_epi_ab,
          "opt": lambda r: bench_gemm(r, OPT_SHAPES, torch.float16),
+         # vs hipBLASLt (torch.matmul) at micro-batch 12 and 48: TILES=0 for auto only
+         "opt_blas": lambda r: bench_gemm(r, [(f"{n}@M{M}", M, N, K) for M in (6144, 24576)
+                                              for n, N, K in OPT_LAYER], torch.float16),
          "optm": lambda r: bench_dgpt(r, opt_m_cases(), torch.float16),
          "optm_small": lambda r: bench_dgpt(r, opt_m_cases((2048, 4096)), torch.float16),
          "optm_pp": lambda r: bench_dgpt(r, opt_m_cases((2048, 6144)), torch.float16)}[k](results)
