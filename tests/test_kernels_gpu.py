@@ -590,6 +590,24 @@ def test_dgrad_epilogue_projection_relu_bwd(tile, dt):
     torch.testing.assert_close(t.float(), ref_t, atol=5e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("tile", [7, 8, 9])
+def test_nontemporal_c_stores_bit_identical(tile, monkeypatch):
+    """MIFT_EPI_NT=1 (non-temporal C stores, the default for outputs >= 96 MiB) writes the same bits as
+    the plain stores, with a residual-dropout epilogue and a ragged last column tile."""
+    from mift.ops import kernels as K_
+    torch.manual_seed(8)
+    M, K, N = 1000, 512, 2560
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    bias = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    res = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    monkeypatch.setenv("MIFT_EPI_NT", "0")
+    ref_out = K_.gemm(a, b, bias, residual=res, dropout_p=0.1, seed=3, tile=tile)
+    monkeypatch.setenv("MIFT_EPI_NT", "1")
+    out = K_.gemm(a, b, bias, residual=res, dropout_p=0.1, seed=3, tile=tile)
+    assert torch.equal(out, ref_out)
+
+
 @pytest.mark.parametrize("tile", [0, 7, 8, 9])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_relu_sign_bits_roundtrip(tile, dt):

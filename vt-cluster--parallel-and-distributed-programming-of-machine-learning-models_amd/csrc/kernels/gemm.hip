@@ -130,6 +130,7 @@ struct EpiArgs {
   // ACT_RELU epilogue, read by ACT_RELU_BWD in place of the 16-bit aux (1/16 of its bytes)
   uint8_t* sbits;
   int pfg;        // 256x256 epilogue: operands requested per group of 4 chunks (MIFT_EPI_PFG, default 1)
+  int ntc;        // non-temporal C stores (outputs >= 96 MiB; MIFT_EPI_NT forces)
 };
 
 // Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
@@ -677,7 +678,12 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         ep.sbits[(size_t)gr * (N >> 3) + (gc >> 3)] = (uint8_t)sb;
       }
       if (ep.lm.dbg & 1) return;  // diagnostics: MIFT_LM_DBG bit 0 skips the C store
-      if (full) store8<T>(C + off, z);
+      if (full && ep.ntc) {  // MIFT_EPI_NT=1 (A/B): non-temporal C stores
+        short8 o;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) { T t = (T)z[e]; short h; __builtin_memcpy(&h, &t, 2); o[e] = h; }
+        __builtin_nontemporal_store(o, reinterpret_cast<short8*>(C + off));
+      } else if (full) store8<T>(C + off, z);
       else for (int e = 0; e < N - gc; ++e) C[off + e] = (T)z[e];
     };
     // ---- epilogue phase 3 (ep.pws): partial T = drop(out tile) · pw[:, n0 : n0+BN]ᵀ over this
@@ -2398,6 +2404,12 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
   {
     const char* e = getenv("MIFT_EPI_PFG");  // read per call (A/B)
     ep.pfg = e ? atoi(e) : 1;
+    // non-temporal C stores for large outputs (OPT-2.7B mb 48, every output 126-503 MB: 4-block step
+    // 302.9 -> 300.7 ms); the distilgpt2 outputs (<= 50 MB) are re-read from the Infinity Cache by the
+    // next kernel (4.872 -> 4.904 ms with NT stores), so the default is by size (profiles/r5/
+    // step_ab_opt_nt*.json, step_ab_dgpt_nt.json).  MIFT_EPI_NT=0 / 1 forces (A/B)
+    const char* n = getenv("MIFT_EPI_NT");
+    ep.ntc = n ? atoi(n) : ((int64_t)M * N * (int64_t)a.element_size() >= (96ll << 20) ? 1 : 0);
   }
   if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);  // diagnostics (bit 0: no C store)
   ep.pre_add = nullptr;
