@@ -47,15 +47,8 @@ def main():
     with open(info, "w") as fh:
         fh.write('extern "C" const char* mift_source_hash() { return "experimental"; }\n')
     srcs.append(info)
-    import hashlib
-    h = hashlib.sha256()
-    for dp, _, fs in sorted(os.walk(SRC)):
-        for f in sorted(fs):
-            if f.endswith((".h", ".hpp")):
-                h.update(open(os.path.join(dp, f), "rb").read())
-    hdr = h.hexdigest()
     with cf.ThreadPoolExecutor(a.jobs) as ex:
-        objs = [o for o, _, _ in ex.map(lambda s: B._compile(s, flags, hdr, False, False, BDIR), srcs)]
+        objs = [o for o, _, _ in ex.map(lambda s: B._compile(s, flags, False, False, BDIR), srcs)]
     _, lib, _ = B._torch_paths()
     cmd = [B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", "-o", OUT + ".tmp"] + objs + [
         f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",

@@ -12,6 +12,7 @@ import argparse
 import concurrent.futures as cf
 import hashlib
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -42,14 +43,31 @@ def _sources():
     return sorted(srcs)
 
 
-def _headers_digest():
+_INCLUDE_RE = re.compile(rb'^[ \t]*#[ \t]*include[ \t]*"([^"]+)"', re.M)
+
+
+def _deps_digest(src):
+    """sha256 over the local files ``src`` includes (``#include "..."``, recursively, resolved against
+    the including file's directory, then csrc/): an object is rebuilt only when something it compiles
+    changed (the GEMM translation units share gemm_impl.h; the other kernels do not see it)."""
     h = hashlib.sha256()
-    for dp, _, fs in os.walk(CSRC):
-        for f in sorted(fs):
-            if f.endswith((".h", ".hpp", ".cuh", ".inc")):
-                with open(os.path.join(dp, f), "rb") as fh:
-                    h.update(f.encode())
-                    h.update(fh.read())
+    seen, todo = set(), [os.path.abspath(src)]
+    while todo:
+        path = todo.pop()
+        with open(path, "rb") as fh:
+            text = fh.read()
+        if path != os.path.abspath(src):
+            h.update(os.path.relpath(path, CSRC).encode())
+            h.update(text)
+        for inc in _INCLUDE_RE.findall(text):
+            name = inc.decode()
+            for base in (os.path.dirname(path), os.path.dirname(os.path.dirname(path)), CSRC):
+                cand = os.path.abspath(os.path.join(base, name))
+                if os.path.exists(cand):
+                    if cand not in seen:
+                        seen.add(cand)
+                        todo.append(cand)
+                    break
     return h.hexdigest()
 
 
@@ -68,7 +86,7 @@ def _common_flags():
     return flags
 
 
-def _compile(src, flags, hdr_digest, force, verbose, build_dir=BUILD_DIR):
+def _compile(src, flags, force, verbose, build_dir=BUILD_DIR):
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_") if src.startswith(CSRC) else os.path.basename(src)
     obj = os.path.join(build_dir, rel + ".o")
     stamp = obj + ".hash"
@@ -76,7 +94,7 @@ def _compile(src, flags, hdr_digest, force, verbose, build_dir=BUILD_DIR):
     with open(src, "rb") as fh:
         h.update(fh.read())
     h.update(" ".join(flags).encode())
-    h.update(hdr_digest.encode())
+    h.update(_deps_digest(src).encode())
     digest = h.hexdigest()
     if not force and os.path.exists(obj) and os.path.exists(stamp):
         with open(stamp) as fh:
@@ -132,12 +150,11 @@ def build(force=False, verbose=False, jobs=None):
     bdir = BUILD_DIR + ("_debug" if debug else "")
     os.makedirs(bdir, exist_ok=True)
     flags = _common_flags()
-    hdr = _headers_digest()
     srcs = _sources() + [_write_build_info(bdir)]
     jobs = jobs or min(16, max(1, (os.cpu_count() or 4)))
     objs, changed = [], False
     with cf.ThreadPoolExecutor(jobs) as ex:
-        futs = [ex.submit(_compile, s, flags, hdr, force, verbose, bdir) for s in srcs]
+        futs = [ex.submit(_compile, s, flags, force, verbose, bdir) for s in srcs]
         for f in futs:
             o, c, _ = f.result()
             objs.append(o)
