@@ -332,10 +332,16 @@ def main():
         epoch_s, epoch_steps = timed_epoch(tr2)
     par = (f"dp{ctx.dp}" + (f"xpp{ctx.pp}" if ctx.pp > 1 else "") + (f"xv{V}" if V > 1 else "")
            + ("+zero1" if a.zero and ctx.dp > 1 else ""))
+    # config_id only when the run IS that BASELINE config (model and pipeline depth); a --model / --pp
+    # override is a custom run and says so instead of borrowing the default config's id
+    base = CONFIGS[a.config]
+    fam = lambda m: "opt" if "opt" in m.lower() else "gpt"  # noqa: E731
+    config_id = a.config if (fam(a.model) == fam(base["model"]) and a.pp == base["pp"]) else None
     if ctx.rank == 0:
-        kind = "PP" if ctx.pp > 1 else "DDP"
+        kind = "PP" if ctx.pp > 1 else ("DDP" if ctx.dp > 1 or config_id is not None else "single-GPU")
         out = {
-            "metric": f"{a.model.split('/')[-1]} LoRA {kind} fine-tune throughput (tokens/sec, whole job, "
+            "metric": ("" if config_id is not None else "custom config: ") +
+                      f"{a.model.split('/')[-1]} LoRA {kind} fine-tune throughput (tokens/sec, whole job, "
                       f"steady state)",
             "value": round(value, 1),
             "unit": "tokens/s",
@@ -348,11 +354,12 @@ def main():
             "vs_baseline": None,
             "dtype": a.precision,
             "data": f"synthetic (OpenWebText-shaped random tokens, full {a.seq_len}-token lines); random-init weights",
-            "config": {"model": a.model, "config_id": a.config, "global_batch": per_rank * ctx.dp,
+            "config": {"model": a.model, "config_id": config_id, "global_batch": per_rank * ctx.dp,
                        "seq_len": a.seq_len, "backend": ctx.backend, "device": ctx.device.type,
                        "parallelism": par, "per_rank_batch": f"{a.batch}x{a.accum}", "micro_batch": f"{mb}x{acc}",
                        "split": split, "lora": "r8/a16/p0.05 " + ",".join(targets), "impl": a.impl,
                        "tokens_per_gpu_per_s": round(value / n, 1), "micro_batch_plan": plan,
+                       "model_override": a.model != base["model"],
                        "final_grad_norm": round(stats["grad_norm"], 4)},
             "wall_clock_epoch_s": epoch_s,
             "epoch": {"lines": a.epoch_lines, "steps": epoch_steps, "global_batch": per_rank * ctx.dp,

@@ -126,8 +126,38 @@ def bench(C, tiles, results):
     print(json.dumps({"t10_ge_blas": wins, "of": len(shapes)}), flush=True)
 
 
+def sweep(C, tiles, results):
+    """K sweep at one chip round of tiles (M = 6144, N = 2560: 240 256x256 tiles): time = per-tile
+    overhead (prologue, epilogue) + K/64 x per-k-tile main-loop time, separated by a linear fit."""
+    for M, N in ((6144, 2560), (4096, 4096)):
+        pts = {}
+        for K in (640, 1280, 2560, 5120, 10240):
+            a, b, _ = operands(M, N, K, torch.float16, scale=False)
+            fns = {f"t{t}": (lambda t=t: gemm(C, a, b, t)) for t in tiles}
+            fns["blas"] = lambda: torch.matmul(a, b.t())
+            ts = {k: [] for k in fns}
+            for _ in range(3):
+                for k, f in fns.items():
+                    ts[k].append(timeit(f, rounds=3))
+            row = {"sweep": f"{M}x{N}", "K": K}
+            for k in fns:
+                row[f"{k}_us"] = round(min(ts[k]) * 1e3, 1)
+                pts.setdefault(k, []).append((K / 64, min(ts[k]) * 1e3))
+            print(json.dumps(row), flush=True)
+            results.append(row)
+        for k, xy in pts.items():
+            n = len(xy)
+            mx = sum(x for x, _ in xy) / n
+            my = sum(y for _, y in xy) / n
+            slope = sum((x - mx) * (y - my) for x, y in xy) / sum((x - mx) ** 2 for x, _ in xy)
+            fit = {"fit": f"{M}x{N}", "variant": k, "us_per_ktile": round(slope, 3), "overhead_us": round(my - slope * mx, 1)}
+            print(json.dumps(fit), flush=True)
+            results.append(fit)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--tiles", default="8,10")
     ap.add_argument("--json", default=None)
@@ -140,7 +170,10 @@ def main():
     if a.check_only or not ok:
         sys.exit(0 if ok else 1)
     results = []
-    bench(C, tiles, results)
+    if a.sweep:
+        sweep(C, tiles, results)
+    else:
+        bench(C, tiles, results)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(results, f, indent=1)

@@ -148,6 +148,9 @@ struct EpiArgs {
   uint8_t* sbits;
   int pfg;        // 256x256 epilogue: operands requested per group of 4 chunks (MIFT_EPI_PFG, default 1)
   int ntc;        // non-temporal C stores (outputs >= 96 MiB; MIFT_EPI_NT forces)
+  // diagnostics (tools/gemm_stamps.py): per block, wave 0's s_memtime at [0] entry, [1] main loop
+  // started (prologue done), [2] main loop done, [3] C tile in LDS, [4] exit; s_memrealtime at [6] / [7]
+  long long* stamps;
 };
 
 // Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
@@ -381,6 +384,13 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / NWN, wn = wave % NWN;
+  auto stamp = [&](int i) {
+    if (ep.stamps != nullptr && tid == 0)
+      ep.stamps[(size_t)blockIdx.x * 8 + i] =
+          i >= 6 ? (long long)__builtin_amdgcn_s_memrealtime() : (long long)__builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
+  stamp(6);
 
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   int m0 = 0, n0 = 0;
@@ -730,6 +740,7 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     sbarrier();
     read_half(0, std::integral_constant<int, 0>{});
     wait_lgkm<0>();
+    stamp(1);
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
@@ -781,35 +792,49 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     T* Cs = reinterpret_cast<T*>(smem);
     using CT = CTile<BN>;
     const float alpha = ep.alpha_ptr != nullptr ? ep.alpha * ep.alpha_ptr[0] : ep.alpha;
+    // acc (+bias, + the dropout-masked K-extension) of fragment column j -> C tile; MASKED is a
+    // compile-time split so the common unmasked body stays a short straight-line block (the 4-wave
+    // tile unrolls 64 fragments: the masked hash inlined into each cost it 36k cycles of I-cache-bound
+    // code per tile, tools/gemm_stamps.py)
+    auto phase1 = [&](auto maskedc) {
+      constexpr bool MASKED = decltype(maskedc)::value;
   #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WN + j * 16 + fq * 4;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (ep.bias != nullptr && n0 + col < N) {
-        if (ep.bias_f32) {
-          float4 t4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ep.bias) + n0 + col);
-          bv[0] = t4.x; bv[1] = t4.y; bv[2] = t4.z; bv[3] = t4.w;
-        } else {
-          load4<T>(reinterpret_cast<const T*>(ep.bias) + n0 + col, bv);
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + fq * 4;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (ep.bias != nullptr && n0 + col < N) {
+          if (ep.bias_f32) {
+            float4 t4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ep.bias) + n0 + col);
+            bv[0] = t4.x; bv[1] = t4.y; bv[2] = t4.z; bv[3] = t4.w;
+          } else {
+            load4<T>(reinterpret_cast<const T*>(ep.bias) + n0 + col, bv);
+          }
+        }
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * WM + i * 16 + fr;
+          float z[4];
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) z[e] = acc[i][j][e] * alpha + bv[e];
+          if (MASKED || (NSTAGE != 1 && ext_masked)) {
+            float4_ xt = mfma16<T>(bf2[j], af2[i], float4_{0.f, 0.f, 0.f, 0.f});
+            bool kp[4];
+            mift_keep4(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col, ep.ext_thr, kp);
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) z[e] += kp[e] ? xt[e] * ep.ext_inv_keep : 0.f;
+          }
+          store4<T>(Cs + CT::off4(row, col), z);
         }
       }
-  #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WM + i * 16 + fr;
-        float z[4];
-  #pragma unroll
-        for (int e = 0; e < 4; ++e) z[e] = acc[i][j][e] * alpha + bv[e];
-        if (ext_masked) {
-          float4_ xt = mfma16<T>(bf2[j], af2[i], float4_{0.f, 0.f, 0.f, 0.f});
-          bool kp[4];
-          mift_keep4(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col, ep.ext_thr, kp);
-  #pragma unroll
-          for (int e = 0; e < 4; ++e) z[e] += kp[e] ? xt[e] * ep.ext_inv_keep : 0.f;
-        }
-        store4<T>(Cs + CT::off4(row, col), z);
-      }
+    };
+    if constexpr (NSTAGE == 1) {
+      if (ext_masked) phase1(std::true_type{});
+      else phase1(std::false_type{});
+    } else {
+      phase1(std::false_type{});  // (the runtime ext_masked test inside, as before)
     }
     __syncthreads();
+    stamp(3);
 
     // ---- epilogue phase 2: 8 columns per thread, 16-B vector I/O, whole rows ----
     // The global operands of ALL this thread's chunks (activation aux, residual) are loaded up
@@ -988,6 +1013,158 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
         }
       }
     };
+    // 4-wave tile (32 chunks per thread, one wave per SIMD): chunks in groups of G, each epilogue
+    // feature applied to the whole group before the next (one uniform branch per feature and group,
+    // the group's loads in flight together) — the per-chunk form ran each chunk's LDS read -> operand
+    // loads -> store as one dependent chain (40k cycles per tile).  Interior tiles only (no bounds
+    // tests); same arithmetic and rounding points as chunk().
+    auto staged = [&]() {
+     if constexpr (NSTAGE == 1) {
+      constexpr int G = 8;
+      static_assert(ITER % G == 0, "chunk groups");
+      const T* pre_add = reinterpret_cast<const T*>(ep.pre_add);
+      const T* auxp = reinterpret_cast<const T*>(ep.aux);
+      const T* resp = reinterpret_cast<const T*>(ep.residual);
+      const bool sb_bwd = ep.act == ACT_RELU_BWD && ep.aux == nullptr && ep.sbits != nullptr;
+      for (int g0 = 0; g0 < ITER; g0 += G) {
+        int row[G], c8[G];
+        size_t off[G];
+        float z[G][8];
+  #pragma unroll
+        for (int k = 0; k < G; ++k) {
+          const int v = tid + (g0 + k) * NT;
+          row[k] = v / VPR;
+          c8[k] = (v % VPR) * 8;
+          off[k] = (size_t)(m0 + row[k]) * ldc + n0 + c8[k];
+          unpack8<T>(CT::read8(Cs, row[k], c8[k]), z[k]);
+        }
+        if (pre_add != nullptr) {
+          short8 pa[G];
+  #pragma unroll
+          for (int k = 0; k < G; ++k) pa[k] = *reinterpret_cast<const short8*>(pre_add + off[k]);
+  #pragma unroll
+          for (int k = 0; k < G; ++k) {
+            float t[8];
+            unpack8<T>(pa[k], t);
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) z[k][e] += t[e];
+          }
+        }
+        if (ep.preact != nullptr) {
+  #pragma unroll
+          for (int k = 0; k < G; ++k) store8<T>(reinterpret_cast<T*>(ep.preact) + off[k], z[k]);
+        }
+        if (sb_bwd) {
+          uint32_t sb[G];
+  #pragma unroll
+          for (int k = 0; k < G; ++k) sb[k] = ep.sbits[(size_t)(m0 + row[k]) * (N >> 3) + ((n0 + c8[k]) >> 3)];
+  #pragma unroll
+          for (int k = 0; k < G; ++k)
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) z[k][e] = (sb[k] >> e) & 1u ? z[k][e] : 0.f;
+        } else if (ep.act != ACT_NONE) {
+          float ax[G][8];
+          if (auxp != nullptr) {
+            short8 av[G];
+  #pragma unroll
+            for (int k = 0; k < G; ++k) av[k] = *reinterpret_cast<const short8*>(auxp + off[k]);
+  #pragma unroll
+            for (int k = 0; k < G; ++k) unpack8<T>(av[k], ax[k]);
+          } else {
+  #pragma unroll
+            for (int k = 0; k < G; ++k)
+  #pragma unroll
+              for (int e = 0; e < 8; ++e) ax[k][e] = 0.f;
+          }
+          switch (ep.act) {
+            case ACT_GELU_TANH:
+  #pragma unroll
+              for (int k = 0; k < G; ++k)
+  #pragma unroll
+                for (int e = 0; e < 8; ++e) z[k][e] = gelu_tanh(z[k][e]);
+              break;
+            case ACT_GELU_TANH_BWD:
+  #pragma unroll
+              for (int k = 0; k < G; ++k)
+  #pragma unroll
+                for (int e = 0; e < 8; ++e) z[k][e] *= gelu_tanh_grad(ax[k][e]);
+              break;
+            case ACT_RELU:
+  #pragma unroll
+              for (int k = 0; k < G; ++k)
+  #pragma unroll
+                for (int e = 0; e < 8; ++e) z[k][e] = fmaxf(z[k][e], 0.f);
+              break;
+            case ACT_RELU_BWD:
+  #pragma unroll
+              for (int k = 0; k < G; ++k)
+  #pragma unroll
+                for (int e = 0; e < 8; ++e) z[k][e] = ax[k][e] > 0.f ? z[k][e] : 0.f;
+              break;
+            default:
+  #pragma unroll
+              for (int k = 0; k < G; ++k)
+  #pragma unroll
+                for (int e = 0; e < 8; ++e) z[k][e] = apply_act(ep.act, z[k][e], ax[k][e]);
+          }
+        }
+        if (ep.thr != 0) {
+  #pragma unroll
+          for (int k = 0; k < G; ++k) {
+            bool kp[8];
+            mift_keep8(ep.seed, (uint64_t)(m0 + row[k]) * N + n0 + c8[k], ep.thr, kp);
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) z[k][e] = kp[e] ? z[k][e] * ep.inv_keep : 0.f;
+          }
+        }
+        if (resp != nullptr) {
+          short8 rv[G];
+  #pragma unroll
+          for (int k = 0; k < G; ++k) rv[k] = *reinterpret_cast<const short8*>(resp + off[k]);
+  #pragma unroll
+          for (int k = 0; k < G; ++k) {
+            float t[8];
+            unpack8<T>(rv[k], t);
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) z[k][e] += t[e];
+          }
+        }
+        short8 o[G];
+  #pragma unroll
+        for (int k = 0; k < G; ++k)
+  #pragma unroll
+          for (int e = 0; e < 8; ++e) { T t = (T)z[k][e]; short h; __builtin_memcpy(&h, &t, 2); o[k][e] = h; }
+        if (ep.pws != nullptr) {
+  #pragma unroll
+          for (int k = 0; k < G; ++k) CT::write8(Cs, row[k], c8[k], o[k]);
+        }
+        if (ep.sbits != nullptr && ep.act == ACT_RELU) {
+  #pragma unroll
+          for (int k = 0; k < G; ++k) {
+            uint32_t sb = 0;
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) sb |= ((float)(T)z[k][e] > 0.f ? 1u : 0u) << e;
+            ep.sbits[(size_t)(m0 + row[k]) * (N >> 3) + ((n0 + c8[k]) >> 3)] = (uint8_t)sb;
+          }
+        }
+        if (ep.lm.dbg & 1) continue;
+        if (ep.ntc) {
+  #pragma unroll
+          for (int k = 0; k < G; ++k) __builtin_nontemporal_store(o[k], reinterpret_cast<short8*>(C + off[k]));
+        } else {
+  #pragma unroll
+          for (int k = 0; k < G; ++k) *reinterpret_cast<short8*>(C + off[k]) = o[k];
+        }
+      }
+     }
+    };
+    if constexpr (NSTAGE == 1) {
+      if (m0 + BM <= M && n0 + BN <= N) {
+        staged();
+        if (ep.pws != nullptr) proj_phase();
+        return;
+      }
+    }
     if constexpr (PF_OK) {
       if (!ep.prefetch) {
         for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{}, -1);
@@ -1302,7 +1479,10 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     } else {
       mainloop(0, nk_all);
     }
+    stamp(2);
     epilogue();
+    stamp(4);
+    stamp(7);
     return;
   } else {
     // ---- split-K tail (separate instantiation: its bookkeeping must not cost the DP kernel
@@ -2233,7 +2413,16 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     const long n256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
     const long t96 = (long)((M + 127) / 128) * ((N + 95) / 96);
-    if ((K >= 1024 && n256 >= 128) || n256 >= 2048) tile = 8;
+    if ((K >= 1024 && n256 >= 128) || n256 >= 2048) {
+      // the 4-wave loop (tile 10) beats the phased 8-wave one on plain and bias / ReLU / gelu / LoRA
+      // K-extension epilogues (OPT layer GEMMs 1-7 % plain, qkv / fc1 forward 7-11 % at M 2048-4096),
+      // but one wave per SIMD cannot hide the dependent hash chains of a dropout mask: with a residual
+      // dropout or a masked K-extension tile 8 stays faster (out / fc2 / dgrads, 4-19 %;
+      // profiles/r6/bench_gemm4_epilogues.json).  MIFT_GEMM_T10=0 / 1 forces either (read per call, A/B)
+      const char* e = getenv("MIFT_GEMM_T10");
+      const bool hashes = ep.thr != 0 || ep.ext_thr != 0;
+      tile = (e ? atoi(e) != 0 : !hashes) ? 10 : 8;
+    }
     // one chip-wave of 128x96 tiles (1-2 per CU): the OPT micro-batch-4 shapes (M = 2048, N = 2560)
     // ran 20-30 % faster than on the 128x256 split-K / 128x128 tiles (fc2 fwd 167 -> 122 us, qkv dgrad
     // 134 -> 94, out proj 50 -> 40; profiles/r4/bench_tiles_opt_pp_microbatch.json)
@@ -2606,6 +2795,15 @@ at::Tensor mift_lmhead_dgrad(const at::Tensor& E, const at::Tensor& wt, const at
 #endif  // MIFT_GEMM_PART == 3
 
 #if MIFT_GEMM_PART == 0
+// diagnostics: every later gemm_nt launch records per-block cycle stamps into buf (int64 [blocks, 8]),
+// None turns it off (tools/gemm_stamps.py)
+static long long* g_gemm_stamps = nullptr;
+void mift_gemm_set_stamps(const c10::optional<at::Tensor>& buf) {
+  TORCH_CHECK(!buf || (buf->is_cuda() && buf->scalar_type() == at::kLong && buf->is_contiguous()),
+              "gemm_set_stamps: int64 GPU buffer");
+  g_gemm_stamps = buf ? reinterpret_cast<long long*>(buf->data_ptr<int64_t>()) : nullptr;
+}
+
 // out = epi(a @ b^T [+ a2 @ b2^T]).  a:[M,K], b:[N,K] (K-contiguous, K%64==0).
 std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
                                      const c10::optional<at::Tensor>& a2, const c10::optional<at::Tensor>& b2,
@@ -2709,6 +2907,7 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     ep.pout = proj.data_ptr();
     ep.palpha = (float)proj_alpha * (proj_p > 0 ? mift_inv_keep(proj_p) : 1.f);
   }
+  ep.stamps = g_gemm_stamps;
   ep.sbits = nullptr;
   if (sbits) {  // ReLU sign bits: written (act = relu) or read in place of aux (act = relu backward)
     TORCH_CHECK((act == ACT_RELU || (act == ACT_RELU_BWD && !aux)) && N % 8 == 0 && sbits->is_cuda() &&

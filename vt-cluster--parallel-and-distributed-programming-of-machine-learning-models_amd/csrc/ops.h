@@ -96,6 +96,7 @@ at::Tensor mift_attn_bwd_bits(const at::Tensor& dout, const at::Tensor& qkv, con
                               const c10::optional<at::Tensor>& kv_len, const c10::optional<at::Tensor>& bits);
 
 // ---- K12 decode attention over a KV cache (kernels/decode.hip)
+void mift_gemm_set_stamps(const c10::optional<at::Tensor>& buf);
 bool mift_gemm_ln_ok(int64_t M, int64_t N, int64_t K);
 std::vector<at::Tensor> mift_gemm_ln(const at::Tensor& x, const at::Tensor& ln_w, const at::Tensor& ln_b, double eps,
                                      const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
@@ -110,6 +111,7 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
                             int64_t gend, const c10::optional<at::Tensor>& t_dev);
 
 #define MIFT_BIND_MORE(m) \
+  m.def("gemm_set_stamps", &mift_gemm_set_stamps, "diagnostics: per-block cycle stamps of later gemm_nt launches"); \
   m.def("gemm_ln_ok", &mift_gemm_ln_ok, "shapes the LN-prologue skinny GEMM takes"); \
   m.def("gemm_ln", &mift_gemm_ln, "act(LN(x) w^T + bias) for M <= 64 rows (decode), LN applied in the GEMM"); \
   m.def("gemm_ln_fold", &mift_gemm_ln_fold, "act(rstd (x wf^T - mean c1) + c2): LN folded into the weights (decode)"); \
