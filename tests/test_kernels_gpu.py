@@ -528,11 +528,13 @@ def test_gemm_tiles_splitk_tail_fused(tile, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (1000, 704, 640),
                                    (2048, 2560, 2560), (777, 2304, 704)])
 @pytest.mark.parametrize("epi", ["plain", "fwd", "relu_bits", "dgrad_masked", "gelu_pre"])
-def test_gemm_4wave_tile_bit_identical_to_phased(dt, M, N, K, epi):
-    """Tile 10 (4-wave 256x256 loop, one to three k-tiles through the steady state, staged epilogue
-    on interior tiles, the generic one on ragged edges) accumulates every output element in the same
-    MFMA order as tile 8 and applies the same epilogue: bit-identical outputs / pre-activations /
-    sign bits for every epilogue family the training step uses."""
+@pytest.mark.parametrize("pair", [(8, 10, "1"), (7, 7, "0"), (9, 9, "0"), (8, 8, "0"), (10, 10, "0")])
+def test_gemm_4wave_tile_and_staged_epilogue_bit_identical(dt, M, N, K, epi, pair, monkeypatch):
+    """(a) Tile 10 (4-wave 256x256 loop, one to three k-tiles through the steady state) accumulates every
+    output element in the same MFMA order as tile 8: bit-identical outputs / pre-activations / sign
+    bits for every epilogue family the training step uses.  (b) The feature-staged epilogue of interior
+    tiles (default) against the per-chunk form (MIFT_EPI_STAGED=0) of the same tile: bit-identical."""
+    ta, tb, staged_a = pair
     from mift.ops import kernels as K_
     C = _C()
     torch.manual_seed(3)
@@ -557,7 +559,10 @@ def test_gemm_4wave_tile_bit_identical_to_phased(dt, M, N, K, epi):
             return list(_gnt(C, a, b, None, a2, b2, 5, aux, None, 0.0, 0, False, 1.0, None, tile, None, None, 0.05, 77))
         return list(_gnt(C, a, b, bias, None, None, 1, None, None, 0.0, 0, True, 1.0, None, tile, None, None, 0.0, 0))
 
-    o8, o10 = run(8), run(10)
+    monkeypatch.setenv("MIFT_EPI_STAGED", staged_a)
+    o8 = run(ta)
+    monkeypatch.setenv("MIFT_EPI_STAGED", "1")
+    o10 = run(tb)
     for x, y in zip(o8, o10):
         if x is not None and x.numel():
             assert torch.equal(x, y)

@@ -151,6 +151,7 @@ struct EpiArgs {
   // diagnostics (tools/gemm_stamps.py): per block, wave 0's s_memtime at [0] entry, [1] main loop
   // started (prologue done), [2] main loop done, [3] C tile in LDS, [4] exit; s_memrealtime at [6] / [7]
   long long* stamps;
+  int staged;     // interior tiles: feature-staged epilogue phase 2 (MIFT_EPI_STAGED, default 1)
 };
 
 // Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
@@ -351,8 +352,23 @@ MIFT_HD void wait_stages(int wave) {
 // fragment read then cover the 16 slots of a bank row once, conflict-free as for KB = 64).  KB = 32
 // keeps the LDS of a 2-stage KB = 64 ring but holds 4 half-depth stages: three k-tiles in flight
 // instead of one for the K = 768 shapes whose main loop waits on LDS-DMA latency.
+// waves per SIMD a tile's LDS footprint allows (launch_gemm's SMEM): the register budget the compiler must
+// respect so that the blocks the LDS admits can actually co-reside (e.g. 128x192: two 8-wave blocks = 4
+// waves per SIMD = 128 VGPRs; without the bound a richer epilogue silently halves the occupancy)
+template <int BM, int BN, int NWM, int NWN, int NSTAGE, int KB>
+constexpr int gemm_waves_per_eu() {
+  constexpr int NT = NWM * NWN * 64;
+  constexpr int RING = (NSTAGE <= 1 ? 2 : NSTAGE) * (BM + BN) * KB * 2;
+  constexpr int CLDU = BN % 64 == 0 ? BN / 4 : 40;
+  constexpr int EPI_BYTES = BM * CLDU * 4 * 2;
+  constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
+  constexpr int BPC = (160 * 1024 / SMEM) < (2048 / NT) ? (160 * 1024 / SMEM) : (2048 / NT);
+  constexpr int W = (BPC > 0 ? BPC : 1) * (NT / 64) / 4;
+  return W > 0 ? W : 1;
+}
+
 template <typename T, int BM, int BN, int NWM, int NWN, int NSTAGE, bool SKM, int EPI = 0, int KB = 64>
-__global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
+__global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN, NSTAGE, KB>())) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                                 T* __restrict__ C, const T* __restrict__ A2,
                                                                 const T* __restrict__ B2, int M, int N, int K,
                                                                 int lda, int ldb, int ldc, EpiArgs ep, SkArgs sk) {
@@ -1019,8 +1035,10 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
     // loads -> store as one dependent chain (40k cycles per tile).  Interior tiles only (no bounds
     // tests); same arithmetic and rounding points as chunk().
     auto staged = [&]() {
-     if constexpr (NSTAGE == 1) {
-      constexpr int G = 8;
+     {
+      // group size: 8 chunks where registers allow; the 8-wave 128-row tiles (two blocks per CU,
+      // <= 128 VGPRs) take groups of 3 / 4
+      constexpr int G = ITER >= 8 ? (NW == 8 && BM == 128 ? 4 : 8) : (ITER % 3 == 0 ? 3 : ITER);
       static_assert(ITER % G == 0, "chunk groups");
       const T* pre_add = reinterpret_cast<const T*>(ep.pre_add);
       const T* auxp = reinterpret_cast<const T*>(ep.aux);
@@ -1158,12 +1176,11 @@ __global__ __launch_bounds__(NWM* NWN * 64) void gemm_nt_kernel(const T* __restr
       }
      }
     };
-    if constexpr (NSTAGE == 1) {
-      if (m0 + BM <= M && n0 + BN <= N) {
-        staged();
-        if (ep.pws != nullptr) proj_phase();
-        return;
-      }
+    // interior tiles: the staged form (every tile; MIFT_EPI_STAGED=0 keeps the per-chunk form, A/B)
+    if (ep.staged && m0 + BM <= M && n0 + BN <= N) {
+      staged();
+      if (ep.pws != nullptr) proj_phase();
+      return;
     }
     if constexpr (PF_OK) {
       if (!ep.prefetch) {
@@ -2908,6 +2925,10 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     ep.palpha = (float)proj_alpha * (proj_p > 0 ? mift_inv_keep(proj_p) : 1.f);
   }
   ep.stamps = g_gemm_stamps;
+  {
+    const char* e = getenv("MIFT_EPI_STAGED");  // read per call (A/B)
+    ep.staged = e ? atoi(e) : 1;
+  }
   ep.sbits = nullptr;
   if (sbits) {  // ReLU sign bits: written (act = relu) or read in place of aux (act = relu backward)
     TORCH_CHECK((act == ACT_RELU || (act == ACT_RELU_BWD && !aux)) && N % 8 == 0 && sbits->is_cuda() &&
