@@ -171,6 +171,27 @@ def test_opt_arena_multi_adapter_matches_dense():
     _grad_close(fused, fused2, 2e-2)
 
 
+def test_pack_lora_multi_matches_torch_pack():
+    """The per-step one-launch pack of the q/k/v adapter group (pack_lora_multi, LoraPack.multi) writes
+    exactly the operands the torch-op construction of MultiAdapterOps builds (s·A rows, B row spans,
+    s·Bᵀ, Aᵀ; zeros elsewhere), for fp16 and bf16."""
+    from mift.lora import LoraArena
+    from mift.lora.pack import attach
+    from mift.ops.fused import MultiAdapterOps
+    for dt in (torch.float16, torch.bfloat16):
+        cfg, ref, fused = _opt_models(dt, 0.1, 0.05)
+        arena = LoraArena(fused)
+        with torch.no_grad():
+            arena.param.copy_(torch.randn_like(arena.param))
+        cat = fused.model.decoder.layers[1].self_attn.qkv
+        a = MultiAdapterOps(cat, dt)  # no pack attached: torch ops
+        attach(fused, arena, dt)
+        cat._mpack = None
+        b = MultiAdapterOps(cat, dt)  # LoraPack.multi
+        for x, y in ((a.A32s, b.A32s), (a.B32, b.B32), (a.B32t, b.B32t), (a.At32, b.At32)):
+            assert x.shape == y.shape and torch.equal(x, y)
+
+
 def test_fused_backward_notifies_dp_reducer_per_layer(monkeypatch):
     """DDP overlap on the fused path (mift.ops.fused._notify -> arena.grad_ready, which the DP
     reducer turns into bucket all-reduces): a fake reducer records the order of notifications

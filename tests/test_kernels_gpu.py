@@ -854,3 +854,25 @@ def test_ln_bwd_mask_proj_matches_separate_passes(D, rank, p, dres, wf32, dt):
     keep = (y0 != 0) | (dh0 == 0)
     torch.testing.assert_close((pr.float()[:, :rank]), (0.5 * y.float() @ pw.float()[:rank].t()), atol=3e-2, rtol=2e-2)
     assert keep.all() if p == 0 else True
+
+
+@pytest.mark.parametrize("S", [7, 256, 700])
+def test_mask_positions_matches_torch(S):
+    """mask_positions (one launch) == HF-style cumsum(mask)·mask - 1 and Σ mask, for right-, left- and
+    middle-padded int64 masks, S below / at / above one 256-token chunk."""
+    from mift.models.opt import opt_positions
+    from mift.ops import kernels as K_
+    torch.manual_seed(1)
+    B = 9
+    mask = torch.ones(B, S, dtype=torch.int64, device="cuda")
+    for b in range(B):
+        n = int(torch.randint(0, S + 1, (1,)))
+        if b % 3 == 0:
+            mask[b, n:] = 0       # right padding
+        elif b % 3 == 1:
+            mask[b, :S - n] = 0   # left padding
+        else:
+            mask[b] = (torch.rand(S, device="cuda") > 0.3).long()
+    pos, kv = K_.mask_positions(mask)
+    assert torch.equal(pos, opt_positions(mask))
+    assert torch.equal(kv, mask.sum(1, dtype=torch.int32))

@@ -108,6 +108,38 @@ __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ 
   }
 }
 
+// OPT's learned positions and key lengths from the attention mask, one block per row:
+// pos[b, t] = cumsum(mask[b])[t]·mask[b, t] - 1 (HF OPTLearnedPositionalEmbedding; pad -> -1) and
+// kv_len[b] = Σ_t mask[b, t] — one launch in place of the six torch kernels (cumsum, mul, sub, cast,
+// sum) the replayed OPT step ran per micro-batch.  Chunks of 256 tokens, block-wide inclusive scan
+// (wave shuffles + one LDS word per wave), running carry.
+__global__ __launch_bounds__(256) void mask_positions_kernel(const int64_t* __restrict__ mask, int S,
+                                                             int64_t* __restrict__ pos, int* __restrict__ kv_len) {
+  __shared__ int wsum[4];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t* m = mask + (int64_t)b * S;
+  int carry = 0;
+  for (int t0 = 0; t0 < S; t0 += 256) {
+    const int t = t0 + threadIdx.x;
+    const int v = t < S ? (int)m[t] : 0;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int before = carry;
+    for (int k = 0; k < w; ++k) before += wsum[k];
+    const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (t < S) pos[(int64_t)b * S + t] = (int64_t)(before + x) * v - 1;
+    carry += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) kv_len[b] = carry;
+}
+
 template <typename T>
 __global__ void pack_lora_kernel(const float* __restrict__ A, const float* __restrict__ B, T* __restrict__ A32,
                                  T* __restrict__ B32, int r, int K, int N, float a_scale) {
@@ -185,6 +217,18 @@ at::Tensor mift_embed_fwd(const at::Tensor& ids, const c10::optional<at::Tensor>
                              (uint64_t)seed, mift_seed_step(), thr_of(p), inv, (int64_t)wte.size(0),
                              wpe ? (int64_t)wpe->size(0) : (int64_t)0));
   return h;
+}
+
+std::vector<at::Tensor> mift_mask_positions(const at::Tensor& mask) {
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kLong && mask.dim() == 2 && mask.is_contiguous(),
+              "mask_positions: int64 [B, S] contiguous mask");
+  const int B = mask.size(0), S = mask.size(1);
+  auto pos = at::empty({B, S}, mask.options());
+  auto kv = at::empty({B}, mask.options().dtype(at::kInt));
+  if (B == 0 || S == 0) return {pos, kv};
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  mask_positions_kernel<<<B, 256, 0, st>>>(mask.data_ptr<int64_t>(), S, pos.data_ptr<int64_t>(), kv.data_ptr<int>());
+  return {pos, kv};
 }
 
 std::vector<at::Tensor> mift_pack_lora(const at::Tensor& A, const at::Tensor& B, double a_scale,

@@ -1404,6 +1404,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
       mainloop8(w0 * GK, min(nk_all, w1 * GK), [&](int kt) {
         const int gk = w0 * GK + kt;
         if (gk % GK != 0) return;
+        if (lm.dbg & 8) return;  // diagnostics (MIFT_LM_DBG bit 3): no rescale — wrong numbers, timing only
         const int g = gk / GK - w0;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {

@@ -847,6 +847,71 @@ __global__ __launch_bounds__(256) void pack_lora_all_kernel(const float* __restr
 }
 }  // namespace
 
+// ------------------------------------------------------------ pack_lora_multi
+// The shared-input adapter groups (OPT's q/k/v as one [3d, d] GEMM, ops/fused.py MultiAdapterOps):
+// adapter j of a group owns rank columns [q_j, q_j + r_j) of the 32 and output rows [n0_j, n1_j).
+// Group g's operands (one buffer, address in its table row): A32s [32,K] (s_j·A_j in rows q_j..),
+// B32 [N,32] (B_j in its row span / rank columns), B32t [32,N] (s_j·B_jᵀ), At32 [K,32] (A_jᵀ); zeros
+// elsewhere.  One launch per optimizer step for every group (the torch-op form ran ~22 kernels per
+// layer inside the replayed OPT step: zero fills, scaled slice copies, casts).
+//   table[g] = {K, N, nslots, out_ptr, then per slot j < 4: r, q, n0, n1, offA, offB};  scales[g][j]
+constexpr int MULTI_COLS = 4 + 4 * 6;
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void pack_lora_multi_kernel(const float* __restrict__ arena,
+                                                              const int64_t* __restrict__ table,
+                                                              const float* __restrict__ scales) {
+  const int64_t* t = table + (int64_t)blockIdx.y * MULTI_COLS;
+  const int K = (int)t[0], N = (int)t[1], ns = (int)t[2];
+  T* o = reinterpret_cast<T*>(t[3]);
+  const float* sc = scales + blockIdx.y * 4;
+  const int64_t nA = 32LL * K, nB = 32LL * N;
+  const int64_t total = 2 * nA + 2 * nB;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    int rk, other;  // rank column (0..31), and the row index along K or N
+    int part;       // 0 A32s, 1 B32, 2 B32t, 3 At32
+    if (i < nA) { part = 0; rk = (int)(i / K); other = (int)(i % K); }
+    else if (i < nA + nB) { const int64_t j = i - nA; part = 1; other = (int)(j / 32); rk = (int)(j % 32); }
+    else if (i < nA + 2 * nB) { const int64_t j = i - nA - nB; part = 2; rk = (int)(j / N); other = (int)(j % N); }
+    else { const int64_t j = i - nA - 2 * nB; part = 3; other = (int)(j / 32); rk = (int)(j % 32); }
+    float v = 0.f;
+    for (int s = 0; s < ns; ++s) {
+      const int64_t* u = t + 4 + 6 * s;
+      const int r = (int)u[0], q = (int)u[1], n0 = (int)u[2], n1 = (int)u[3];
+      if (rk < q || rk >= q + r) continue;
+      const float* A = arena + u[4];
+      const float* B = arena + u[5];
+      if (part == 0) v = A[(int64_t)(rk - q) * K + other] * sc[s];
+      else if (part == 3) v = A[(int64_t)(rk - q) * K + other];
+      else if (other >= n0 && other < n1) {
+        const float b = B[(int64_t)(other - n0) * r + (rk - q)];
+        v = part == 1 ? b : b * sc[s];
+      }
+      break;
+    }
+    o[i] = (T)v;
+  }
+}
+}  // namespace
+
+void mift_pack_lora_multi(const at::Tensor& arena, const at::Tensor& table, const at::Tensor& scales,
+                          int64_t max_elems, bool bf16_out) {
+  TORCH_CHECK(arena.scalar_type() == at::kFloat && table.scalar_type() == at::kLong &&
+                  table.size(1) == MULTI_COLS && scales.scalar_type() == at::kFloat && scales.numel() == table.size(0) * 4,
+              "pack_lora_multi: arena fp32, table int64 [g, 28], scales fp32 [g, 4]");
+  const int n = table.size(0);
+  if (n == 0) return;
+  hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+  const int gx = (int)std::min<int64_t>(512, (max_elems + 255) / 256);
+  dim3 grid(gx, n);
+  if (bf16_out)
+    pack_lora_multi_kernel<bf16><<<grid, 256, 0, st>>>(arena.data_ptr<float>(), table.data_ptr<int64_t>(),
+                                                       scales.data_ptr<float>());
+  else
+    pack_lora_multi_kernel<fp16><<<grid, 256, 0, st>>>(arena.data_ptr<float>(), table.data_ptr<int64_t>(),
+                                                       scales.data_ptr<float>());
+}
+
 void mift_pack_lora_all(const at::Tensor& arena, const at::Tensor& table, const at::Tensor& scales, at::Tensor& out,
                         int64_t max_elems) {
   TORCH_CHECK(arena.scalar_type() == at::kFloat && table.scalar_type() == at::kLong && table.size(1) == 6,

@@ -42,6 +42,8 @@ void mift_lora_wgrad_group(at::Tensor& out, const std::vector<at::Tensor>& xs, c
                            const std::vector<int64_t>& meta, const std::vector<double>& ps);
 void mift_pack_lora_all(const at::Tensor& arena, const at::Tensor& table, const at::Tensor& scales, at::Tensor& out,
                         int64_t max_elems);
+void mift_pack_lora_multi(const at::Tensor& arena, const at::Tensor& table, const at::Tensor& scales,
+                          int64_t max_elems, bool bf16_out);
 
 // ---- row producers fused with the LoRA projection (kernels/rowproj.hip)
 std::vector<at::Tensor> mift_layer_norm_fwd_proj(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
@@ -59,6 +61,7 @@ std::vector<at::Tensor> mift_mask_proj(const at::Tensor& x, double p, int64_t se
 at::Tensor mift_mask_scale(const at::Tensor& x, double p, int64_t seed, const c10::optional<at::Tensor>& out,
                            bool accumulate);
 at::Tensor mift_act_bwd(const at::Tensor& g, const at::Tensor& z, int64_t act, double p, int64_t seed);
+std::vector<at::Tensor> mift_mask_positions(const at::Tensor& mask);
 at::Tensor mift_embed_fwd(const at::Tensor& ids, const c10::optional<at::Tensor>& pos, const at::Tensor& wte,
                           const c10::optional<at::Tensor>& wpe, int64_t pos_offset, double p, int64_t seed,
                           at::ScalarType out_dtype);
@@ -125,6 +128,7 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
   m.def("ln_bwd_mask_proj", &mift_ln_bwd_mask_proj, "dh = LN-bwd + dres, y = dropout-bwd(dh), proj = alpha*y@pw^T"); \
   m.def("lora_wgrad", &mift_lora_wgrad, "out[P,32] += drop(x)^T @ y (tr_b16 split-M MFMA); arena modes"); \
   m.def("lora_wgrad_group", &mift_lora_wgrad_group, "grouped LoRA weight grads (<= 16 problems, one launch)"); \
+  m.def("pack_lora_multi", &mift_pack_lora_multi, "one-launch pack of every shared-input adapter group (q/k/v)"); \
   m.def("pack_lora_all", &mift_pack_lora_all, "pack every adapter's 16-bit operands from the fp32 arena"); \
   m.def("attn_fwd", &mift_attn_fwd, "causal flash attention fwd on fused qkv -> (o, lse)"); \
   m.def("attn_bwd", &mift_attn_bwd, "causal flash attention bwd -> dqkv"); \
@@ -148,6 +152,7 @@ at::Tensor mift_decode_attn(const at::Tensor& qkv, at::Tensor& kc, at::Tensor& v
   m.def("opt_apply", &mift_opt_apply, "AdamW [+ finalize from all-reduced stats] (zeroes grads)"); \
   m.def("mask_scale", &mift_mask_scale, "counter-hash dropout (fwd == bwd), optional accumulate"); \
   m.def("act_bwd", &mift_act_bwd, "dz = dropmask(g) * act'(z)"); \
+  m.def("mask_positions", &mift_mask_positions, "OPT positions cumsum(mask)*mask-1 and key lengths, one launch"); \
   m.def("embed_fwd", &mift_embed_fwd, "token + position gather (+dropout)"); \
   m.def("pack_lora", &mift_pack_lora, "fp32 LoRA A,B -> padded 16-bit A32[32,K], B32[N,32]"); \
   m.def("xent_fwd_bwd", &mift_xent_fwd_bwd, "row cross-entropy; dlogits written in place");

@@ -41,11 +41,49 @@ class LoraPack:
             m._pack = (A32s, B32, B32t, At32)
             m._pack_owner = self
         self.version = -1
+        # shared-input adapter groups (ops.fused.MultiAdapterOps, e.g. OPT q/k/v): registered on first
+        # use (an eager pass: the Trainer's warm-up precedes any capture), packed by one launch per step
+        self.groups = {}
+        self.mtable = self.mscales = None
+        self.mmax = 0
 
     def refresh(self, force=False):
         if force or self.version != self.arena.version:
             C().pack_lora_all(self.arena.param, self.table, self.scales, self.buf, self.max_elems)
+            if self.groups:
+                C().pack_lora_multi(self.arena.param, self.mtable, self.mscales, self.mmax,
+                                    self.dtype == torch.bfloat16)
             self.version = self.arena.version
+
+    def multi(self, key, K, N, slots):
+        """Views (A32s [32,K], B32 [N,32], B32t [32,N], At32 [K,32]) of the group ``key`` whose adapters
+        are ``slots`` = [(lin, n0, n1, q)] (rank columns [q, q + r), output rows [n0, n1)); its operands
+        are rebuilt with every other adapter's by ``refresh``."""
+        g = self.groups.get(key)
+        if g is None:
+            assert len(slots) <= 4, "pack_lora_multi: at most 4 adapters per group"
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("LoraPack.multi: first use of an adapter group inside a graph capture")
+            dev = self.arena.param.device
+            buf = torch.zeros(64 * (K + N), dtype=self.dtype, device=dev)
+            row = [K, N, len(slots), buf.data_ptr()]
+            sc = []
+            for lin, n0, n1, q in slots:
+                row += [lin.lora_r, q, n0, n1, lin._offA, lin._offB]
+                sc.append(lin.lora_scaling)
+            row += [0] * (28 - len(row))
+            sc += [0.0] * (4 - len(sc))
+            views = (buf[:32 * K].view(32, K), buf[32 * K:32 * (K + N)].view(N, 32),
+                     buf[32 * (K + N):32 * (K + 2 * N)].view(32, N), buf[32 * (K + 2 * N):].view(K, 32))
+            g = self.groups[key] = (buf, views, row, sc)
+            rows = [v[2] for v in self.groups.values()]
+            self.mtable = torch.tensor(rows, dtype=torch.int64, device=dev)
+            self.mscales = torch.tensor([v[3] for v in self.groups.values()], dtype=torch.float32, device=dev)
+            self.mmax = max(self.mmax, 64 * (K + N))
+            self.refresh(force=True)
+        else:
+            self.refresh()
+        return g[1]
 
 
 def attach(model, arena, dtype):

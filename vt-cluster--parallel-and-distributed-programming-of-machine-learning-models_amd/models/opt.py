@@ -278,10 +278,15 @@ class OPTForCausalLM(CausalLMBase):
         from ..ops import kernels as K
         cfg, training = self.config, self.training
         dec = self.model.decoder
-        kv_len = attention_mask.sum(1, dtype=torch.int32) if attention_mask is not None else None
+        pos = kv_len = None
+        if attention_mask is not None:
+            if attention_mask.dtype == torch.int64 and attention_mask.is_contiguous():
+                pos, kv_len = K.mask_positions(attention_mask)  # one launch for both
+            else:
+                kv_len = attention_mask.sum(1, dtype=torch.int32)
+                pos = opt_positions(attention_mask).contiguous()
         if self.embed_here:
             B, S = input_ids.shape
-            pos = opt_positions(attention_mask).contiguous() if attention_mask is not None else None
             h = K.embed(input_ids.contiguous(), dec.embed_tokens.weight, dec.embed_positions.weight, pos=pos,
                         pos_offset=OPTLearnedPositionalEmbedding.OFFSET).view(B, S, -1)
         else:

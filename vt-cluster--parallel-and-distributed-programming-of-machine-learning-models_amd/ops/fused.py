@@ -287,6 +287,12 @@ class MultiAdapterOps:
         self.arena = getattr(first, "_arena", None)
         if self.arena is not None:
             _claim(self.arena, [o for l, _, _, _ in self.slots for o in (l._offA, l._offB)])
+        pk = getattr(first, "_pack_owner", None)
+        if pk is not None and pk.dtype == dtype and self.arena is not None:
+            # the model-level pack: one pack_lora_multi launch per step for every group (no torch ops)
+            self.A32s, self.B32, self.B32t, self.At32 = pk.multi(
+                id(cat), cat.in_features, cat.out_features, [(l, n0, n1, q) for l, n0, n1, q in self.slots])
+            return
         key = (self.arena.version if self.arena is not None else None, dtype, _PACK_GEN[0])
         cached = getattr(cat, "_mpack", None)
         if self.arena is not None and cached is not None and cached[0] == key:

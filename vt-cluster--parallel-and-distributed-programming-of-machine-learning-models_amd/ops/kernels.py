@@ -99,6 +99,11 @@ def embed(ids, wte, wpe=None, pos=None, pos_offset=0, p=0.0, seed=0):
     return C().embed_fwd(ids, pos, wte, wpe, int(pos_offset), float(p), int(seed), wte.dtype)
 
 
+def mask_positions(mask):
+    """(cumsum(mask)·mask - 1 [B, S] int64, Σ mask [B] int32) of an int64 [B, S] attention mask."""
+    return C().mask_positions(mask)
+
+
 def pack_lora(A, B, a_scale, dtype):
     return C().pack_lora(A, B, float(a_scale), dtype)
 
