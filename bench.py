@@ -182,10 +182,11 @@ def main():
     if a.pp > 1 and (a.micro_batch == "auto" or a.virtual == "auto"):
         # micro-batch and interleaving depth from the measured dp1 cost curve (before the grid is built:
         # interleaving needs the wrap-around links)
-        from mift.parallel.plan import choose_micro_batch
+        from mift.parallel.plan import choose_micro_batch, stage_graphs_expected
         cands = None if a.micro_batch == "auto" else [int(a.micro_batch)]
         plan = choose_micro_batch(mcfg, a.seq_len, per_rank, a.pp, dtype_bytes=2, name=a.model, candidates=cands,
-                                  virtual="auto" if a.virtual == "auto" else int(a.virtual))
+                                  virtual="auto" if a.virtual == "auto" else int(a.virtual),
+                                  graphed=stage_graphs_expected(fused=a.impl == "fused" and a.device != "cpu"))
         a.micro_batch, a.virtual = str(plan["micro_batch"]), str(plan["virtual"])
     V = int(a.virtual)
     ctx = D.init(pp=a.pp, verbose=False, sanity=True, virtual=V)

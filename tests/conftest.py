@@ -30,3 +30,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _destroy_process_groups():
+    """Tests that form a single-process world (gloo / RCCL, world 1) leave the default group alive for
+    the next test; tear it down once at the end so the run exits without the 'destroy_process_group()
+    was not called' resource-leak warning."""
+    yield
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # pragma: no cover - best effort at interpreter shutdown
+        pass

@@ -190,7 +190,6 @@ def test_flash_attention_whole_sequence_kernels(S, p, dt, monkeypatch):
     """The whole-sequence-in-LDS kernels (MIFT_ATTN_SEQ=2 forces them at this small head count)
     against the fp32 reference, and bit-for-bit agreement of fwd with the tiled kernel."""
     monkeypatch.setenv("MIFT_ATTN_SEQ", "2")
-    monkeypatch.setenv("MIFT_ATTN_FWD", "1")  # bitwise seq-vs-tiled check of the v1 pair (v2: below)
     test_flash_attention_fwd_bwd(64, S, p, dt)
     C = _C()
     B, H, hd = 2, 3, 64
@@ -262,36 +261,6 @@ def test_attention_keep_bits_match_hash(hd, S, dt, monkeypatch):
         torch.testing.assert_close(d_bits, d_hash, atol=0, rtol=0)
         if hd == 64:
             assert bits.numel() == B * H * S * ((S + 63) // 64 * 4)  # the record exists on this path
-
-
-@pytest.mark.parametrize("hd", [64, 80, 128])
-@pytest.mark.parametrize("S", [512, 200])
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_attention_fwd_v2(hd, S, p, monkeypatch):
-    """v2 forward (32x32x16 MFMA, 32 queries per wave, hd 80 QK^T without padding) against the fp32
-    reference incl. right padding, and its keep-bit record (written on the whole-sequence geometry)
-    read by the backward == the re-hashing backward, bit for bit."""
-    monkeypatch.setenv("MIFT_ATTN_FWD", "2")
-    C = _C()
-    torch.manual_seed(3 + hd)
-    B, H = 2, 3
-    dt = torch.float16 if hd == 80 else torch.bfloat16
-    qkv = torch.randn(B * S, 3 * H * hd, device="cuda").to(dt)
-    kvl = torch.tensor([S - 21, S // 3], device="cuda", dtype=torch.int32)
-    for lens in (None, kvl):
-        o, lse = C.attn_fwd(qkv, B, S, H, hd, hd ** -0.5, p, 55, lens)
-        oref = _attn_ref(qkv, B, S, H, hd, hd ** -0.5, p, 55, lens)
-        torch.testing.assert_close(o.float(), oref, atol=3e-2, rtol=3e-2)
-        assert torch.isfinite(lse).all() or lens is not None
-    if p > 0 and S <= 256 or hd == 64:
-        monkeypatch.setenv("MIFT_ATTN_SEQ", "2")
-        for lens in (None, kvl):
-            o, lse, bits = C.attn_fwd_bits(qkv, B, S, H, hd, hd ** -0.5, p, 77, lens)
-            do = torch.randn_like(o)
-            d_hash = C.attn_bwd(do, qkv, o, lse, B, S, H, hd, hd ** -0.5, p, 77, lens)
-            d_bits = C.attn_bwd_bits(do, qkv, o, lse, B, S, H, hd, hd ** -0.5, p, 77, lens,
-                                     bits if bits.numel() else None)
-            torch.testing.assert_close(d_bits, d_hash, atol=0, rtol=0)
 
 
 def test_flash_attention_kv_len():
@@ -401,37 +370,6 @@ def test_lora_wgrad_group_deterministic(det, monkeypatch):
     assert outs[0][:64].eq(0.25).all() and outs[0][64 + 8 * K:].eq(0.25).all()
     for o in outs[1:]:
         assert torch.equal(o, outs[0]), "deterministic wgrad must be bit-reproducible"
-
-
-@pytest.mark.parametrize("qoff,rank", [(0, 8), (8, 16)])
-def test_lora_wgrad_in_kernel_reduction_matches_separate_launch(qoff, rank, monkeypatch):
-    """Opt-in MIFT_WGRAD_FIN=1: the last chunk block of every column tile reduces its slabs in chunk
-    order (one launch); the default separate reduction launch adds the same slabs in the same order: equal bits,
-    over a grouped launch of dB (mode 1) and multi-slot dA (mode 2) problems; repeated launches keep
-    the self-re-arming tile counters consistent."""
-    C = _C()
-    torch.manual_seed(6)
-    M = 8192
-    xs = [torch.randn(M, P, device="cuda", dtype=torch.bfloat16) for P in (2304, 768, 3072)]
-    ys = [torch.randn(M, 32, device="cuda", dtype=torch.bfloat16) for _ in xs]
-    n = 64 + sum(rank * x.shape[1] for x in xs) + 4096
-    offs, o = [], 64
-    for x in xs:
-        offs.append(o)
-        o += rank * x.shape[1]
-    meta = []
-    for i, x in enumerate(xs):
-        meta += [1 if i != 1 else 2, 1, qoff, rank, offs[i]] + [0, 0, 0] * 3 + [11 + i]
-    res = {}
-    for fin in ("1", "0", "1"):
-        monkeypatch.setenv("MIFT_WGRAD_FIN", fin)
-        arena = torch.full((n,), 0.5, device="cuda")
-        C.lora_wgrad_group(arena, xs, ys, meta, [0.0, 0.05, 0.0])
-        res.setdefault(fin, []).append(arena)
-    assert torch.equal(res["1"][0], res["0"][0]) and torch.equal(res["1"][1], res["0"][0])
-    exp = (xs[0].float().t() @ ys[0].float()[:, qoff:qoff + rank]).reshape(-1) + 0.5  # dB layout [P, rank]
-    got = res["1"][0][offs[0]:offs[0] + rank * xs[0].shape[1]]
-    assert ((got - exp).norm() / exp.norm()).item() < 1e-2
 
 
 def test_grad_stats_deterministic():

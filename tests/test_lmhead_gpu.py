@@ -140,29 +140,6 @@ def test_lmhead_in_launch_total_ignore_and_gmul():
     assert torch.equal(d1, d2)
 
 
-@pytest.mark.parametrize("split", ["0", "8", "3"])
-def test_lmhead_dgrad_in_launch_reduction_bit_identical(monkeypatch, split):
-    """The dgrad's in-launch reduction (each tile's last chunk block sums the write-through slabs,
-    subtracts W[label] and applies g x gmul) gives the bits of the separate lmhead_reduce launch, for
-    several split counts, with ignored rows and a gradient multiplier; repeated calls re-arm the
-    per-tile counters."""
-    V, dtype, ign = 50257, torch.bfloat16, -100
-    h, ln, W, lab, Vp = _case(V, dtype, ign, M=1000)
-    a, _, _ = K.layer_norm_fwd(h, ln.weight, ln.bias, ln.eps)
-    E, stats, lse, loss, zlab = K.lmhead_fwd(a, W, lab, V)
-    Wt = W.t().contiguous()
-    s = torch.tensor([512.0], device="cuda")
-    m = torch.tensor([1.0 / 977.0], device="cuda")
-    if split != "0":
-        monkeypatch.setenv("MIFT_LM_SPLIT", split)
-    monkeypatch.setenv("MIFT_LM_FIN", "0")  # the default (the in-launch form is opt-in: measured slower)
-    ref = K.lmhead_dgrad(E, Wt, W, lab, V, stats, lse, s, 0, -1, m)
-    monkeypatch.setenv("MIFT_LM_FIN", "1")
-    for _ in range(3):
-        out = K.lmhead_dgrad(E, Wt, W, lab, V, stats, lse, s, 0, -1, m)
-        assert torch.equal(out, ref)
-
-
 @pytest.mark.parametrize("V,dtype,ignore,shift", [(50257, torch.bfloat16, -100, 128), (50272, torch.float16, 1, 0)])
 def test_lmhead_chunked_matches_whole(V, dtype, ignore, shift, monkeypatch):
     """MIFT_LM_CHUNK (SURVEY K7's chunked head: each chunk's E consumed by its dgrad inside forward, no

@@ -105,7 +105,8 @@ OPT_CASES = [  # OPT-2.7B at micro-batch 48 x 512 tokens, fp16
 
 
 def bench_epi_ab(results):
-    """Epilogue prefetch A/B (MIFT_EPI_PREFETCH 0 vs 1) interleaved in one process (guide rule 24)."""
+    """Epilogue form A/B (MIFT_EPI_STAGED 0 = per-chunk, 1 = feature-staged) interleaved in one process
+    (guide rule 24)."""
     import mift._C as C
     for name, M, N, K, e in DGPT_CASES + OPT_CASES:
         dt = torch.float16 if name.startswith("opt") else torch.bfloat16
@@ -121,10 +122,10 @@ def bench_epi_ab(results):
         ts = {0: [], 1: []}
         for _ in range(3):
             for pf in (0, 1):
-                os.environ["MIFT_EPI_PREFETCH"] = str(pf)
+                os.environ["MIFT_EPI_STAGED"] = str(pf)
                 ts[pf].append(timeit(fn, rounds=3))
-        os.environ.pop("MIFT_EPI_PREFETCH", None)
-        row = {"name": name, "pf0_us": round(min(ts[0]) * 1e3, 1), "pf1_us": round(min(ts[1]) * 1e3, 1)}
+        os.environ.pop("MIFT_EPI_STAGED", None)
+        row = {"name": name, "per_chunk_us": round(min(ts[0]) * 1e3, 1), "staged_us": round(min(ts[1]) * 1e3, 1)}
         print(json.dumps(row), flush=True)
         results.append(row)
 

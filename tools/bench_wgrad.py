@@ -1,7 +1,7 @@
 """Grouped LoRA weight-gradient launch at the distilgpt2 per-layer shapes (the 6 dB/dA problems of
 one transformer layer in ONE lora_wgrad_group call), same-process interleaved A/B of env knobs.
 
-  python tools/bench_wgrad.py "MIFT_WGRAD_V=1" "MIFT_WGRAD_V=2" [--p 0.05]
+  python tools/bench_wgrad.py "MIFT_WGRAD_BLOCKS=1024" "MIFT_WGRAD_BLOCKS=2048" [--p 0.05]
 Also checks every arm against the first one (max |diff| of the accumulated arena).
 """
 import argparse

@@ -121,11 +121,12 @@ def plan_micro_batch(args, ds, stages, world, gpu):
     plan = None
     if stages > 1 and (mbsel == "auto" or vsel == "auto"):
         from ..models.opt import OPTConfig
-        from ..parallel.plan import choose_micro_batch
+        from ..parallel.plan import choose_micro_batch, stage_graphs_expected
         cfg = OPTConfig.preset(args.model_name)
+        rec = bool(getattr(args, "gradient_checkpointing", False)) or bool(getattr(ds, "activation_checkpointing", False))
         plan = choose_micro_batch(cfg, args.seq_len, per_step, stages, dtype_bytes=2, name=args.model_name,
                                   candidates=None if mbsel == "auto" else [mbsel or base_mb],
-                                  virtual=vsel)
+                                  virtual=vsel, graphed=stage_graphs_expected(recompute=rec))
         mbsel, vsel = plan["micro_batch"], plan["virtual"]
     elif mbsel == "auto":
         mbsel = 0

@@ -1314,268 +1314,9 @@ __global__ __launch_bounds__(NW * 64, HD <= 64 ? 4 : 2) void attn_bwd_dkdv_seq_k
   }
 }
 
-// ===================== forward v2: 32x32x16 MFMA, 32 queries per wave =====================
-// Structure of cdna_hip_programming.md App. B "Fused attention prefill" (swapped QK^T, P as the
-// PV operand with no lane movement), sized for these shapes:
-//   * each wave owns 32 queries; NW waves per block (128 queries at NW = 4, two blocks per CU);
-//   * QK^T per 64-key tile: S^T[32 keys x 32 queries] = K · Q^T (v_mfma_f32_32x32x16) over
-//     HD/16 k-steps, twice (keys 0-31, 32-63): head dim 80 runs EXACTLY 5 k-steps (the v1 kernel
-//     zero-padded QK^T to 96: +20 % MFMAs);  A = K rows (ds_read_b128 of an odd-16-B-stride image:
-//     conflict-free), B = Q rows straight from global into registers (16 B per lane per k-step);
-//   * each lane then holds 32 of its query's 64 scores (lane l and l^32 the other 32): row max /
-//     sum need one xor-32 shuffle; lazy rescale (running max moves only by > 2^8);
-//   * O^T[hd x q] += V^T · P^T: the score accumulator registers 8(s&1)..8(s&1)+7 of chain s>>1
-//     ARE the B operand of k-step s (guide §3 "An accumulator tile as the next MFMA's operand",
-//     permuted k order); the V^T operand = two ds_read_b64_tr_b16 of the row-major V image
-//     (stride = 64 or 192 mod 256 B: conflict-free per 32-lane half).  O^T keeps the query on the
-//     lane, so the online-softmax rescale and the final 1/l are per-lane multiplies.  hd 80 runs
-//     PV as 3 blocks of 32 columns (the image's columns 80-95 are zero).
-//   * 32x32x16 reads 1 KB of LDS per 32-cycle MFMA (16x16x32: per 16 cycles): half the LDS bytes
-//     per FLOP of the v1 kernel.
-// Same contracts as v1: causal + right-padding kv_len, counter-hash dropout (identical masks),
-// lse in natural log, optional keep-bit record in the whole-sequence layout (KEEP BITS).
-MIFT_HD float16_ mfma32(bf16x8 a, bf16x8 b, float16_ c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-MIFT_HD float16_ mfma32(fp16x8 a, fp16x8 b, float16_ c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
-
-template <int HD>
-struct Geo2 {
-  static constexpr int NKS = HD / 16;            // QK^T k-steps of 16
-  static constexpr int NOB = (HD + 31) / 32;     // PV output blocks of 32 head columns
-  static constexpr int HDV = NOB * 32;           // V image columns (zero padded past HD)
-  static constexpr int KRS = ((HD * 2) / 16 | 1) * 16;  // K image stride: odd multiple of 16 B
-  static constexpr int VRS = (HDV * 2) % 256 == 64 || (HDV * 2) % 256 == 192 ? HDV * 2 : HDV * 2 + 64;
-  static_assert(VRS % 256 == 64 || VRS % 256 == 192, "V image stride: 4 rows on distinct 64-B windows");
-  static constexpr int K_BYTES = 64 * KRS, V_BYTES = 64 * VRS;
-  static constexpr int CH = HD / 8;              // 16-B chunks per global row
-};
-
-template <typename T, int HD, int NW>
-__global__ __launch_bounds__(NW * 64, HD <= 80 ? 2 : 1) void attn_fwd2_kernel(const T* __restrict__ qkv, T* __restrict__ out,
-                                                            float* __restrict__ lse, const int* __restrict__ kv_len,
-                                                            int B, int S, int H, float scale, uint64_t seed,
-                                                            const int64_t* __restrict__ sstep, uint32_t thr,
-                                                            float inv_keep, uint16_t* __restrict__ dmask, int xcd) {
-  seed = mift_seed(seed, sstep);
-  using G = Geo2<HD>;
-  constexpr int NT = NW * 64;
-  constexpr int BQB = 32 * NW;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Ks = smem;
-  char* Vs = smem + G::K_BYTES;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hh = lane >> 5, qi = lane & 31;
-  const int nqt = (S + BQB - 1) / BQB;
-  const int bid = attn_block_id(xcd);
-  const int qt = nqt - 1 - (bid % nqt);  // heavy (late) query tiles first
-  const int bh = bid / nqt;
-  const int b = bh / H, h = bh % H;
-  const int D = H * HD;
-  const int64_t ld = 3LL * D;
-  const T* Qg = qkv + (int64_t)b * S * ld + h * HD;
-  const T* Kg = Qg + D;
-  const T* Vg = Qg + 2 * D;
-  const int klen = kv_len ? kv_len[b] : S;
-  MIFT_ASSERT(klen >= 0 && klen <= S);
-  const int q0 = qt * BQB + wave * 32;
-  const int myq = q0 + qi;
-  const float c2 = scale * LOG2E;
-  const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
-  const uint32_t hm0 = mift_hmix(seed, 0);
-  const int SPW = (S + 63) / 64 * 4;  // keep-bit record elements per query
-
-  // Q^T fragments (B operand): lane -> query q0 + (lane & 31), head dims 16s + 8h .. +7
-  vec8<T> qf[G::NKS];
-  {
-    const int gq = min(myq, S - 1);
-#pragma unroll
-    for (int s = 0; s < G::NKS; ++s)
-      qf[s] = *reinterpret_cast<const vec8<T>*>(Qg + (int64_t)gq * ld + 16 * s + 8 * hh);
-  }
-  // zero the V image's padding columns [HD, HDV) once (never overwritten by the tile stores)
-  if constexpr (G::HDV != HD) {
-    for (int i = tid; i < 64 * (G::HDV - HD) / 8; i += NT) {
-      const int r = i / ((G::HDV - HD) / 8), c = HD / 8 + i % ((G::HDV - HD) / 8);
-      *reinterpret_cast<short8*>(Vs + r * G::VRS + c * 16) = short8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  }
-
-  float m = -INFINITY, l = 0.f;
-  float16_ o[G::NOB];
-#pragma unroll
-  for (int i = 0; i < G::NOB; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
-
-  const int kend = min((qt + 1) * BQB, klen);
-  const int nkt = (kend + 63) / 64;
-  constexpr int NCH = (64 * G::CH + NT - 1) / NT;  // 16-B chunks per thread per tile and operand
-  short8 kr[NCH], vr[NCH];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int i = tid + u * NT;
-      if ((64 * G::CH) % NT == 0 || i < 64 * G::CH) {
-        const int r = i / G::CH, c = i % G::CH;
-        const int gr = min(k0 + r, S - 1);
-        kr[u] = *reinterpret_cast<const short8*>(Kg + (int64_t)gr * ld + c * 8);
-        vr[u] = *reinterpret_cast<const short8*>(Vg + (int64_t)gr * ld + c * 8);
-      }
-    }
-  };
-  auto lstore = [&]() {
-#pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int i = tid + u * NT;
-      if ((64 * G::CH) % NT == 0 || i < 64 * G::CH) {
-        const int r = i / G::CH, c = i % G::CH;
-        *reinterpret_cast<short8*>(Ks + r * G::KRS + c * 16) = kr[u];
-        *reinterpret_cast<short8*>(Vs + r * G::VRS + c * 16) = vr[u];
-      }
-    }
-  };
-  if (nkt > 0) gload(0);
-  // V^T operand address of this lane: tr-read block rows 16s + 4h + (li >> 2) (+8), columns
-  // 32·ob + 16·(lane >> 4 & 1) + 4·(li & 3)
-  const int li = lane & 15;
-  const int vcol = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
-  const int vrow = 4 * hh + (li >> 2);
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int k0 = kt * 64;
-    __syncthreads();  // the previous tile's LDS readers are done
-    lstore();
-    __syncthreads();
-    if (kt + 1 < nkt) gload(k0 + 64);  // next tile in flight during this tile's math
-    if (k0 > q0 + 31) continue;       // none of this wave's queries sees the tile (wave-uniform)
-    float16_ st[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st[c][r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < G::NKS; ++s) {
-        const vec8<T> kf = ld_frag<T>(Ks + (32 * c + qi) * G::KRS + (16 * s + 8 * hh) * 2);
-        st[c] = mfma32(kf, qf[s], st[c]);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // one chain's K fragments live at a time (VGPR budget)
-    }
-    // scores of key k0 + 32c + (r & 3) + 8 (r >> 2) + 4 hh for query myq
-    const bool diag = (k0 + 63 > q0) || (k0 + 64 > klen);
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = st[c][r] * c2;
-        if (diag) {
-          const int key = k0 + 32 * c + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (key > myq || key >= klen) v = -INFINITY;
-        }
-        st[c][r] = v;
-        tmax = fmaxf(tmax, v);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const bool resc = __any(tmax > m + 8.f);
-    float alpha = 1.f;
-    if (resc) {
-      const float mnew = fmaxf(m, tmax);
-      alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mnew);
-      m = mnew;
-    }
-    vec8<T> pf[4];
-    float psum = 0.f;
-    uint32_t kb[2] = {0u, 0u};  // keep bits: element 2c + (r >> 3) of the tile, bit 8((r>>2)&1) + 4hh + (r&3)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {  // 4 consecutive keys k0 + 32c + 8 r4 + 4hh + 0..3
-        bool kp[4] = {true, true, true, true};
-        if (thr != 0) {
-          const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + 32 * c + 8 * r4 + 4 * hh;
-          if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
-          else mift_keep4(seed, i0, thr, kp);
-          const uint32_t nib = (uint32_t)kp[0] | ((uint32_t)kp[1] << 1) | ((uint32_t)kp[2] << 2) | ((uint32_t)kp[3] << 3);
-          kb[c] |= nib << (16 * (r4 >> 1) + 8 * (r4 & 1) + 4 * hh);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * r4 + e;
-          float pv = (m == -INFINITY) ? 0.f : fast_exp2(st[c][r] - m);
-          psum += pv;
-          if (thr != 0) pv = kp[e] ? pv * inv_keep : 0.f;
-          pf[2 * c + (r >> 3)][r & 7] = (T)pv;
-        }
-      }
-    if (dmask != nullptr) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c) kb[c] |= __shfl_xor(kb[c], 32, 64);
-      if (hh == 0 && myq < S) {
-        uint16_t* rec = dmask + ((int64_t)bh * S + myq) * SPW + kt * 4;
-        rec[0] = (uint16_t)(kb[0] & 0xFFFF);
-        rec[1] = (uint16_t)(kb[0] >> 16);
-        rec[2] = (uint16_t)(kb[1] & 0xFFFF);
-        rec[3] = (uint16_t)(kb[1] >> 16);
-      }
-    }
-    l = l * alpha + psum;
-    if (resc) {
-#pragma unroll
-      for (int i = 0; i < G::NOB; ++i) o[i] *= alpha;
-    }
-#pragma unroll
-    for (int ob = 0; ob < G::NOB; ++ob)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int off = (16 * s + vrow) * G::VRS + (32 * ob + vcol) * 2;
-        v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Vs + off));
-        v4s c8 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)(Vs + off + 8 * G::VRS));
-        short8 t = {a[0], a[1], a[2], a[3], c8[0], c8[1], c8[2], c8[3]};
-        vec8<T> vf;
-        __builtin_memcpy(&vf, &t, 16);
-        o[ob] = mfma32(vf, pf[s], o[ob]);
-        if (s == 3) __builtin_amdgcn_sched_barrier(0);  // one output block's V^T fragments at a time
-      }
-  }
-  // finish: l over the query's two lanes; O^T row (hd) = 32 ob + (r & 3) + 8 (r >> 2) + 4 hh
-  const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv_l = lt > 0.f ? 1.f / lt : 0.f;
-  if (hh == 0 && myq < S) lse[(int64_t)bh * S + myq] = (lt > 0.f) ? (m + log2f(lt)) * LN2 : -INFINITY;
-  if (myq < S) {
-    T* Og = out + ((int64_t)b * S + myq) * D + h * HD;
-#pragma unroll
-    for (int ob = 0; ob < G::NOB; ++ob)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int col = 32 * ob + 8 * r4 + 4 * hh;
-        if (col < HD) {
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = o[ob][4 * r4 + e] * inv_l;
-          store4<T>(Og + col, v);
-        }
-      }
-  }
-}
-
-// MIFT_ATTN_FWD (read per call, A/B-able): 2 = the v2 kernel (head dims 64/80/128), else v1.
-// v2 is opt-in: measured SLOWER than v1 on every model shape (tools/bench_attn.py, MI355X:
-// distilgpt2 33.4 vs 27.2 us, OPT-2.7B 65.5 vs 62.1 us, OPT-6.7B 192 vs 159 us; profiles/r3/
-// bench_attn_v1_v2.txt) — register pressure (hd 128: 343 VGPR -> one wave per SIMD) and two
-// barriers per 64-key tile with only 4-8 waves per CU; kept (tested) for the record.
-// v2 forward (32x32x16, opt-in MIFT_ATTN_FWD=2): with the XCD-aware tile mapping too it stays behind v1
-// (OPT-2.7B 57.0 vs 49.6 us, OPT-6.7B 168 vs 117, distilgpt2 31.8 vs 23.1;
-// profiles/r5/bench_attn_fwd_v1_v2_xcd.json)
-bool attn_fwd_v2(int hd, bool seq) {
-  (void)seq;
-  const char* e = getenv("MIFT_ATTN_FWD");
-  return hd != 32 && e != nullptr && atoi(e) == 2;
-}
-
+// (A 32x32x16 forward with 32 queries per wave, "v2", was measured slower than this one on every
+// model shape in rounds 3 and 5 — profiles/r3/bench_attn_v1_v2.txt, profiles/r5/bench_attn_fwd_v1_v2_xcd.json —
+// and removed in round 6.)
 template <typename T, int HD>
 void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int* kvl, int B, int S, int H, float scale,
                 uint64_t seed, uint32_t thr, float inv_keep, hipStream_t st, uint16_t* dmask) {
@@ -1591,18 +1332,6 @@ void fwd_launch(const at::Tensor& qkv, at::Tensor& o, at::Tensor& lse, const int
   const int SP = (S + BKV - 1) / BKV * BKV;
   const int seq_smem = SP * seq_row_bytes<HD>();
   const bool seq = seq_env && 2 * seq_smem <= 160 * 1024 && (B * H >= 256 || seq_env == 2);
-  if (attn_fwd_v2(HD, seq)) {
-    // v2 (32x32x16, 32 queries per wave); writes the keep-bit record when the whole-sequence
-    // backward expects it (the record layout depends only on the launch geometry)
-    constexpr int NW = 4;
-    using G2 = Geo2<HD>;
-    const int nqt = (S + 32 * NW - 1) / (32 * NW);
-    hipLaunchKernelGGL((attn_fwd2_kernel<T, HD, NW>), dim3(B * H * nqt), dim3(NW * 64), G2::K_BYTES + G2::V_BYTES,
-                       st, (const T*)qkv.data_ptr(), (T*)o.data_ptr(), lse.data_ptr<float>(), kvl, B, S, H, scale,
-                       seed, mift_seed_step(), thr, inv_keep, (seq && thr != 0) ? dmask : nullptr,
-                       seq ? 0 : attn_xcd_env());
-    return;
-  }
   // transposed-output P·V (read per call: A/B): on for the whole-sequence kernel (distilgpt2 fwd 23.3 ->
   // 22.8 us), off for the tiled one (OPT-2.7B 49.2 vs 49.9 us, OPT-6.7B 115.9 vs 118.5;
   // profiles/r5/bench_attn_ot_xcd.jsonl)

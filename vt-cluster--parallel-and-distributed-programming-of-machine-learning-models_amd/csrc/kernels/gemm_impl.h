@@ -92,16 +92,8 @@ struct LmArgs {
   int gpc;                // groups per split-K chunk
   float* partial;         // [S][M][N] fp32 split-K slabs
   int dbg;                // MIFT_LM_DBG (diagnostics only): bit 0 = skip the E store, bit 2 = no FULL-tile epilogue
-  int nt;                 // MIFT_LM_NT (A/B): bit 0 = nontemporal E stores (fwd), bit 1 = nt E loads (dgrad)
   int shift;              // > 0: labels are the UNSHIFTED [B*S] ids, S = shift (see lm_label)
   int64_t ignore;         // >= 0: this id is no target (OPT ignores its pad id, a real vocabulary entry)
-  // dgrad in-launch reduction (fin != nullptr): the chunk blocks of a tile store their slabs write-through
-  // and the last to arrive (counter fin[tile]) applies lmhead_reduce_kernel's arithmetic to the tile
-  unsigned* fin;
-  const float* gmul;      // optional 1/tokens of a replayed step
-  const void* w;          // [V_pad, N] (rows = the one-hot part W[label])
-  int ldw;
-  void* dx;               // [M, N] output
 };
 
 // Target of row `row`: with shift = S the labels tensor holds the unshifted ids and row r's target
@@ -130,7 +122,6 @@ struct EpiArgs {
   uint64_t ext_seed;
   float ext_inv_keep;
   const int64_t* sstep;    // device micro-step for graph-replayed dropout seeds (common.h mift_seed)
-  int prefetch;            // epilogue: load aux / residual of all chunks up front (MIFT_EPI_PREFETCH=1; opt-in)
   int group_m;             // tile raster: 0 = row panels (n fastest); g > 0 = groups of g row panels, m fastest
   // LoRA input projection of the OUTPUT (T = s·drop(out)·Aᵀ for the next layer's adapter, e.g. GPT-2
   // mlp.c_proj's input f = gelu(c_fc(x))): pw = A32s [32, N] (s baked in), the first prow rows
@@ -540,10 +531,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
         const int r = i * 8 + srow;
         const int gr = min(r00 + r, rmax);
         const void* src = (const void*)(G + (size_t)gr * ld + (kb + t) * BK + (spc ^ (r & 7)) * 8);
-        if ((EPI == 2 || EPI == 4) && o == 0 && (ep.lm.nt & 2))  // E is streamed once: keep W resident in L2
-          __builtin_amdgcn_global_load_lds(src, (void*)(base + i * 1024), 16, 0, 2);
-        else
-          __builtin_amdgcn_global_load_lds(src, (void*)(base + i * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(src, (void*)(base + i * 1024), 16, 0, 0);
       }
     };
     const int arow = wm * WM + fr, brow = wn * WN + fr;
@@ -860,23 +848,10 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
     constexpr int VPR = BN / 8;
     constexpr int ITER = BM * VPR / NT;
     static_assert((BM * VPR) % NT == 0, "epilogue chunks must split evenly over the threads");
-    // Measured: -2..8 % per GEMM in isolation on the 128x96 / 128x128 tiles but +1.5 % on the
-    // distilgpt2 step (same-device A/B), +2..5 % slower on the 256x256 tile (16 chunks per thread
-    // per operand burst at once): opt-in (MIFT_EPI_PREFETCH=1), small tiles only.  The default
-    // loop stays rolled: unrolling it with the generic activation switch cost the 256x256 ReLU
-    // epilogues 20 % (OPT fc1 fwd 1395 -> 1121 us, fc2 dgrad 1594 -> 1321 us at M = 24576).
+    // (an up-front operand prefetch for all chunks, MIFT_EPI_PREFETCH, measured +1.5 % on the distilgpt2
+    // step and +2..5 % on the 256x256 tile, rounds 2 / 5, and was removed in round 6; interior tiles
+    // take the staged form below)
     constexpr bool PF_OK = ITER <= 8;
-    // MIFT_EPI_PREFETCH: 1 = aux and residual, 2 = residual only
-    const bool pf_aux = PF_OK && ep.prefetch == 1 && ep.aux != nullptr && ep.act != ACT_NONE && N >= 8;
-    const bool pf_res = PF_OK && ep.prefetch != 0 && ep.residual != nullptr && N >= 8;
-    auto prefetch = [&](const void* src, short8* dst) {
-  #pragma unroll
-      for (int it = 0; it < ITER; ++it) {
-        const int v = tid + it * NT;
-        const int gr = min(m0 + v / VPR, M - 1), gc = min(n0 + (v % VPR) * 8, N - 8);
-        dst[it] = *reinterpret_cast<const short8*>(reinterpret_cast<const T*>(src) + (size_t)gr * ldc + gc);
-      }
-    };
     // one 8-column chunk: (aux, res) come prefetched when have_aux / have_res
     auto chunk = [&](int it, bool have_aux, short8 auxv, bool have_res, short8 resv, int sbp) {
       const int v = tid + it * NT;
@@ -1183,15 +1158,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
       return;
     }
     if constexpr (PF_OK) {
-      if (!ep.prefetch) {
-        for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{}, -1);
-      } else {
-        short8 aux_r[ITER], res_r[ITER];
-        if (pf_aux) prefetch(ep.aux, aux_r);
-        if (pf_res) prefetch(ep.residual, res_r);
-  #pragma unroll
-        for (int it = 0; it < ITER; ++it) chunk(it, pf_aux, aux_r[it], pf_res, res_r[it], -1);
-      }
+      for (int it = 0; it < ITER; ++it) chunk(it, false, short8{}, false, short8{}, -1);
     } else {
       // 256x256 (16 chunks per thread, one block per CU: no second block hides a chunk's operand round
       // trip, ~1 us from HBM, paid 16 times per tile in the rolled loop — OPT's residual-dropout
@@ -1328,8 +1295,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
       const int gr = m0 + r, gc = n0 + c8;
       if (gr < M && gc < N) {
         const short8 ev = CT::read8(Cs, r, c8);
-        if (lm.nt & 1) __builtin_nontemporal_store(ev, reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc));
-        else *reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc) = ev;
+        *reinterpret_cast<short8*>(C + (size_t)gr * ldc + gc) = ev;
       }
     }
   };
@@ -1363,7 +1329,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
       lm_fwd_epilogue();
     }
     return;
-  } else if constexpr (EPI == 2 || EPI == 4) {  // 4: + the in-launch reduction (opt-in, MIFT_LM_FIN=1)
+  } else if constexpr (EPI == 2) {
     // ---- LM-head dgrad on the phased 256x256 tile.  A = E [M, V_pad], B = Wᵀ [N, V_pad].
     // Each group of GK k-tiles is one forward column tile j whose E is relative to its own max
     // m_j.  Flash-style, acc is kept relative to a per-row reference ref: at every group start
@@ -1418,7 +1384,6 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
       });
     }
     float* dst = lm.partial + (size_t)cidx * M * N;
-    constexpr bool fin = EPI == 4;  // a separate instantiation: the default kernel carries none of it
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = m0 + wm * WM + i * 16 + fr;
@@ -1427,48 +1392,8 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + wn * WN + j * 16 + fq * 4;
-        if (col < N) {
-          if (fin)  // byte offset < 2^31 (host-checked)
-            mift_st16_sc1(lm.partial, (uint32_t)((((size_t)cidx * M + row) * N + col) * 4), acc[i][j] * fac);
-          else
-            *reinterpret_cast<float4_*>(dst + (size_t)row * N + col) = acc[i][j] * fac;
-        }
+        if (col < N) *reinterpret_cast<float4_*>(dst + (size_t)row * N + col) = acc[i][j] * fac;
       }
-    }
-    if constexpr (!fin) return;
-    __shared__ int lm_last;
-    if (!mift_group_arrival(lm.fin + tl, (unsigned)S, &lm_last)) return;
-    // the tile's last chunk block: slabs summed in chunk order, one-hot part, upstream gradient — the
-    // arithmetic of lmhead_reduce_kernel (bit-identical), without its launch and its cold re-read
-    const float gsc = lm.gmul ? lm.gscale[0] * lm.gmul[0] : lm.gscale[0];
-    const T* wl = reinterpret_cast<const T*>(lm.w);
-    T* dxo = reinterpret_cast<T*>(lm.dx);
-    constexpr int CPT = BN / 8;
-    for (int v = tid; v < BM * CPT; v += NT) {
-      const int row = m0 + v / CPT, c8 = n0 + (v % CPT) * 8;
-      if (row >= M || c8 >= N) continue;
-      float a8[8];
-      {
-        const float4* p = reinterpret_cast<const float4*>(lm.partial + (size_t)row * N + c8);
-        const float4 a = p[0], b = p[1];
-        a8[0] = a.x; a8[1] = a.y; a8[2] = a.z; a8[3] = a.w; a8[4] = b.x; a8[5] = b.y; a8[6] = b.z; a8[7] = b.w;
-      }
-      for (int q = 1; q < S; ++q) {
-        const float4* p = reinterpret_cast<const float4*>(lm.partial + ((size_t)q * M + row) * N + c8);
-        const float4 a = p[0], b = p[1];
-        a8[0] += a.x; a8[1] += a.y; a8[2] += a.z; a8[3] += a.w; a8[4] += b.x; a8[5] += b.y; a8[6] += b.z; a8[7] += b.w;
-      }
-      const int64_t lab = lm_label(lm.labels, row, lm.shift, lm.ignore);
-      if (lab >= 0 && lab < lm.V) {
-        float wv[8];
-        load8<T>(wl + (size_t)lab * lm.ldw + c8, wv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a8[e] = gsc * (a8[e] - wv[e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a8[e] = 0.f;
-      }
-      store8<T>(dxo + (size_t)row * N + c8, a8);
     }
     return;
   } else if constexpr (!SKM) {
@@ -2600,7 +2525,6 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   ep.lm.shift = shift;
   ep.lm.ignore = ignore;
   if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);
-  if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   {
     // tile raster of the head: the 32 blocks an XCD runs at once cover g row panels x 32/g vocab tiles,
     // so each W tile is fetched from the Infinity Cache once per g row panels (row-panel order, g = 1,
@@ -2662,15 +2586,6 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
   return {E, stats, lse, loss, zlab};
 }
 
-// per-tile arrival counters of the LM-head dgrad's in-launch reduction (zeroed once, re-armed by each
-// tile's last chunk block; first allocated by an eager call, outside any capture)
-unsigned* lm_fin_flags(int n) {
-  static at::Tensor flags;
-  if (!flags.defined() || flags.numel() < n)
-    flags = at::zeros({std::max<int64_t>(n, 1 << 12)}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA));
-  return reinterpret_cast<unsigned*>(flags.data_ptr<int>());
-}
-
 template <typename T>
 at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at::Tensor& w, const at::Tensor& labels,
                              int V, const at::Tensor& stats, const at::Tensor& lse, const at::Tensor& gscale, int shift,
@@ -2701,35 +2616,19 @@ at::Tensor lmhead_dgrad_impl(const at::Tensor& E, const at::Tensor& wt, const at
   ep.lm.partial = partial.data_ptr<float>();
   ep.lm.shift = shift;
   ep.lm.ignore = ignore;
-  if (const char* d = getenv("MIFT_LM_NT")) ep.lm.nt = atoi(d);
   SkArgs sk{};
   auto kern2 = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 2>;
-  auto kern4 = gemm_nt_kernel<T, BM, BN, 2, 4, 0, false, 4>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern2, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    (void)hipFuncSetAttribute((const void*)kern4, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr = true;
   }
   hipStream_t st = c10::hip::getCurrentHIPStream().stream();
   auto out = at::empty({M, N}, E.options());
-  // in-launch reduction by each tile's last chunk block: opt-in (MIFT_LM_FIN=1), bit-identical but
-  // slower — distilgpt2 head 1.42 -> 1.59 ms, step +0.17 ms: the 201 MB of write-through slab stores and
-  // the finishers' serial tail cost more than the 37 us launch they replace
-  // (profiles/r4/lmhead_in_launch_reduction_rejected.txt)
-  const char* fe = getenv("MIFT_LM_FIN");
-  const bool fin = fe && atoi(fe) == 1 && (size_t)S * M * N * 4 < (1ull << 31);
-  if (fin) {
-    ep.lm.fin = lm_fin_flags(tiles);
-    ep.lm.gmul = gmul ? gmul->data_ptr<float>() : nullptr;
-    ep.lm.w = w.data_ptr();
-    ep.lm.ldw = (int)w.stride(0);
-    ep.lm.dx = out.data_ptr();
-  }
-  hipLaunchKernelGGL(fin ? kern4 : kern2, dim3(tiles * S), dim3(512), SMEM, st, (const T*)E.data_ptr(),
-                     (const T*)wt.data_ptr(), (T*)nullptr, nullptr, nullptr, M, N, K, (int)E.stride(0),
-                     (int)wt.stride(0), N, ep, sk);
-  if (fin) return out;
+  // (an in-launch reduction by each tile's last chunk block was bit-identical but slower — head 1.42 ->
+  // 1.59 ms, profiles/r4/lmhead_in_launch_reduction_rejected.txt — and was removed in round 6)
+  hipLaunchKernelGGL(kern2, dim3(tiles * S), dim3(512), SMEM, st, (const T*)E.data_ptr(), (const T*)wt.data_ptr(),
+                     (T*)nullptr, nullptr, nullptr, M, N, K, (int)E.stride(0), (int)wt.stride(0), N, ep, sk);
   const size_t chunks = (size_t)M * (N / 8);
   hipLaunchKernelGGL(lmhead_reduce_kernel<T>, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st,
                      partial.data_ptr<float>(), S, M, N, (const T*)w.data_ptr(), (int)w.stride(0),
@@ -2888,10 +2787,6 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
   ep.ext_seed = (uint64_t)ext_seed;
   ep.ext_inv_keep = ext_p > 0 ? mift_inv_keep(ext_p) : 1.f;
   ep.sstep = mift_seed_step();
-  {
-    const char* e = getenv("MIFT_EPI_PREFETCH");  // read per call: A/B-able within one process
-    ep.prefetch = e ? atoi(e) : 0;
-  }
   ep.group_m = gemm_group_m(N);
   {
     const char* e = getenv("MIFT_EPI_PFG");  // read per call (A/B)
@@ -2900,8 +2795,11 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     // 302.9 -> 300.7 ms); the distilgpt2 outputs (<= 50 MB) are re-read from the Infinity Cache by the
     // next kernel (4.872 -> 4.904 ms with NT stores), so the default is by size (profiles/r5/
     // step_ab_opt_nt*.json, step_ab_dgpt_nt.json).  MIFT_EPI_NT=0 / 1 forces (A/B)
+    // threshold at the Infinity Cache size (256 MiB): a smaller output can still be re-read from it by
+    // the next kernel, which NT stores would give up (the 96 MiB form measured +0.7 % on the
+    // mb-48 step, inside the box spread: its gain came from the 503 MB fc1 / fc2-dgrad outputs)
     const char* n = getenv("MIFT_EPI_NT");
-    ep.ntc = n ? atoi(n) : ((int64_t)M * N * (int64_t)a.element_size() >= (96ll << 20) ? 1 : 0);
+    ep.ntc = n ? atoi(n) : ((int64_t)M * N * (int64_t)a.element_size() >= (256ll << 20) ? 1 : 0);
   }
   if (const char* d = getenv("MIFT_LM_DBG")) ep.lm.dbg = atoi(d);  // diagnostics (bit 0: no C store)
   ep.pre_add = nullptr;

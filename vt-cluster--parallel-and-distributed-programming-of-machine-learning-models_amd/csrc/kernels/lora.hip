@@ -220,8 +220,7 @@ struct WgProb {
 struct WgArgs {
   float* out;
   float* ws;        // deterministic mode: [blocks][NQT*16][64] fp32 partial slabs (nullptr: atomics)
-  int* flags;       // per column tile arrival counters (zero, self-re-arming): the last chunk block of a
-                    // tile reduces its slabs in chunk order (nullptr: separate lora_wgrad_reduce launch)
+  int* flags;       // (unused: the slabs are always reduced by lora_wgrad_reduce_kernel)
   const int64_t* sstep;
   int np;
   WgProb p[WG_MAXP];
@@ -241,11 +240,6 @@ template <int NQT>
 MIFT_HD void wg_store(const WgArgs& args, const WgProb& pr, const float4_ (&acc)[NQT], int p0, int wave, int g, int li) {
   if (args.ws != nullptr) {  // deterministic: slab [c][li][64 rows of p], one 16-B store per (c)
     float* slab = args.ws + (size_t)blockIdx.x * (NQT * 16 * 64);
-    if (args.flags != nullptr) {  // in-launch reduction: write-through, handed to the tile's last block
-#pragma unroll
-      for (int c = 0; c < NQT; ++c) mift_st16_sc1(slab, ((c * 16 + li) * 64 + wave * 16 + g * 4) * 4, acc[c]);
-      return;
-    }
 #pragma unroll
     for (int c = 0; c < NQT; ++c)
       *reinterpret_cast<float4_*>(slab + (c * 16 + li) * 64 + wave * 16 + g * 4) = acc[c];
@@ -268,123 +262,11 @@ MIFT_HD void wg_store(const WgArgs& args, const WgProb& pr, const float4_ (&acc)
 template <int NQT>
 MIFT_HD void wg_reduce_tile(const WgArgs& args, const WgProb& pr, int pt);
 
-template <typename T>
-__global__ __launch_bounds__(256) void lora_wgrad_kernel(const WgArgs args) {
-  int pi = 0;
-#pragma unroll 1
-  while (pi + 1 < args.np && (int)blockIdx.x >= args.p[pi + 1].blk0) ++pi;
-  const WgProb& pr = args.p[pi];
-  const T* __restrict__ X = reinterpret_cast<const T*>(pr.X);
-  const T* __restrict__ Y = reinterpret_cast<const T*>(pr.Y);
-  const int M = pr.M, P = pr.P, ldx = pr.ldx, rows_per_block = pr.rows;
-  const uint32_t thr = pr.thr;
-  const float inv_keep = pr.inv_keep;
-  const uint64_t seed = mift_seed(pr.seed, args.sstep);
-  const int lb = blockIdx.x - pr.blk0;
-  // NB 32-row steps per group: the whole group's global loads are in flight
-  // together (one 16-B X load + half a Y load per thread per step), staged
-  // into NB LDS buffers, then consumed; the next group's loads are issued
-  // before this group's transpose reads + MFMAs.
-  constexpr int NB = 4;
-  __shared__ __attribute__((aligned(16))) char Xs[NB][32 * XS];
-  __shared__ __attribute__((aligned(16))) char Ys[NB][32 * YS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
-  const int g = lane >> 4, li = lane & 15;
-  const int ntp = P / 64;
-  const int pt = lb % ntp, ms = lb / ntp;
-  const int p0 = pt * 64;
-  const int mbeg = ms * rows_per_block;
-  const int mend = min(mbeg + rows_per_block, M);
-  MIFT_ASSERT(P % 64 == 0 && mbeg < M);
-  float4_ acc[2] = {float4_{0.f, 0.f, 0.f, 0.f}, float4_{0.f, 0.f, 0.f, 0.f}};
-
-  const int xr = tid >> 3, xc = tid & 7;
-  const int yr = (tid & 127) >> 2, yc = tid & 3;
-  short8 xv[NB], yv[NB];
-  auto gload = [&](int m0g) {
-#pragma unroll
-    for (int s = 0; s < NB; ++s) {
-      const int m = m0g + 32 * s;
-      const int gm = min(m + xr, M - 1);
-      xv[s] = *reinterpret_cast<const short8*>(X + (int64_t)gm * ldx + p0 + xc * 8);
-      if (tid < 128) {
-        const int gy = min(m + yr, M - 1);
-        yv[s] = *reinterpret_cast<const short8*>(Y + (int64_t)gy * 32 + yc * 8);
-      }
-    }
-  };
-  auto lstore = [&](int m0g) {
-#pragma unroll
-    for (int s = 0; s < NB; ++s) {
-      const int m = m0g + 32 * s;
-      const bool valid = (m + xr) < mend;
-      short8 v = xv[s];
-      if (thr != 0 || !valid) {
-        bool kp[8];
-        if (thr != 0) mift_keep8(seed, (uint64_t)min(m + xr, M - 1) * P + p0 + xc * 8, thr, kp);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          short sh = v[e];
-          T t;
-          __builtin_memcpy(&t, &sh, 2);
-          float f = (float)t;
-          f = !valid ? 0.f : (thr != 0 ? (kp[e] ? f * inv_keep : 0.f) : f);
-          t = (T)f;
-          __builtin_memcpy(&sh, &t, 2);
-          v[e] = sh;
-        }
-      }
-      *reinterpret_cast<short8*>(Xs[s] + xr * XS + xc * 16) = v;
-      if (tid < 128) {
-        short8 w = yv[s];
-        if ((m + yr) >= mend) w = short8{0, 0, 0, 0, 0, 0, 0, 0};
-        *reinterpret_cast<short8*>(Ys[s] + yr * YS + yc * 16) = w;
-      }
-    }
-  };
-
-  // transpose-read addresses (permuted rows: first read rows 4g+q', second 16+4g+q')
-  const int q4 = li >> 2, p4 = li & 3;
-  const int rowA = 4 * g + q4;
-  const int xoff = rowA * XS + (wave * 16 + p4 * 4) * 2;
-  const int yoff0 = rowA * YS + (0 * 16 + p4 * 4) * 2;
-  const int yoff1 = rowA * YS + (1 * 16 + p4 * 4) * 2;
-
-  if (mbeg < mend) gload(mbeg);
-  for (int mg = mbeg; mg < mend; mg += 32 * NB) {
-    __syncthreads();
-    lstore(mg);
-    __syncthreads();
-    if (mg + 32 * NB < mend) gload(mg + 32 * NB);
-#pragma unroll
-    for (int s = 0; s < NB; ++s) {
-      if (mg + 32 * s >= mend) break;
-      const char* xb = Xs[s];
-      const char* yb = Ys[s];
-      v4s a0 = tr_read<T>(xb, xoff), a1 = tr_read<T>(xb, xoff + 16 * XS);
-      v4s b00 = tr_read<T>(yb, yoff0), b01 = tr_read<T>(yb, yoff0 + 16 * YS);
-      v4s b10 = tr_read<T>(yb, yoff1), b11 = tr_read<T>(yb, yoff1 + 16 * YS);
-      frag_t<T> af, bf0, bf1;
-      {
-        short8 t = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        __builtin_memcpy(&af, &t, 16);
-        short8 u = {b00[0], b00[1], b00[2], b00[3], b01[0], b01[1], b01[2], b01[3]};
-        __builtin_memcpy(&bf0, &u, 16);
-        short8 w = {b10[0], b10[1], b10[2], b10[3], b11[0], b11[1], b11[2], b11[3]};
-        __builtin_memcpy(&bf1, &w, 16);
-      }
-      acc[0] = mfma16<T>(af, bf0, acc[0]);
-      acc[1] = mfma16<T>(af, bf1, acc[1]);
-    }
-  }
-  wg_store<2>(args, pr, acc, p0, wave, g, li);
-}
-
-// v2 (default; MIFT_WGRAD_V=1 selects the kernel above): the same tiles and LDS images, but two
-// register sets of NB-step load groups alternate, so group g+2's global loads are issued as soon as
-// group g has been written to LDS and group g+1's have had a whole iteration to land (the v1 loop
-// kept ONE group in flight per block: each group paid the full load latency).  NQT = 1 when every
+// Split-M weight gradients: each block reduces a row chunk of one 64-column tile of one problem
+// (X^T·Y over its rows) with MFMA from LDS images of the X and Y row groups.  Two register sets of
+// NB-step load groups alternate, so group g+2's global loads are issued as soon as group g has been
+// written to LDS and group g+1's have had a whole iteration to land (round 2's one-group loop paid the
+// full load latency per group; removed in round 6).  NQT = 1 when every
 // slot of the launch lives in columns [0, 16) (rank <= 16, one adapter per input): one MFMA per
 // 32-row step instead of two and half the Y bytes.
 template <typename T, int NQT>
@@ -512,14 +394,6 @@ __global__ __launch_bounds__(256) void lora_wgrad2_kernel(const WgArgs args) {
     for (int c = 0; c < NQT; ++c) acc[c] *= inv_keep;
   }
   wg_store<NQT>(args, pr, acc, p0, wave, g, li);
-  if (args.flags != nullptr) {  // the last chunk block of this column tile reduces its slabs
-    // write-through slabs + relaxed arrival + one acquire in the last block (common.h); round 3's form
-    // fenced every block (__threadfence in all threads + an acq_rel atomic): step 5.09 -> 6.74 ms
-    __shared__ int last;
-    const int nch = (M + rows_per_block - 1) / rows_per_block;
-    if (mift_group_arrival(reinterpret_cast<unsigned*>(args.flags + pr.tile0 + pt), (unsigned)nch, &last))
-      wg_reduce_tile<NQT>(args, pr, pt);
-  }
 }
 
 // Deterministic reduction: block t = column tile t of the launch (problem pi, tile pt) sums the
@@ -656,12 +530,6 @@ at::Tensor mift_lora_proj(const at::Tensor& x, const at::Tensor& w, double alpha
 namespace {
 // persistent per-column-tile arrival counters of the in-kernel slab reduction (zeroed once; every
 // finisher re-arms its own; first allocated by an eager call, outside any hipGraph capture)
-int* wg_flags(int n) {
-  static at::Tensor flags;
-  if (!flags.defined() || flags.numel() < n)
-    flags = at::zeros({std::max<int64_t>(n, 1 << 14)}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA));
-  return flags.data_ptr<int>();
-}
 
 template <typename T>
 void launch_wgrad(WgArgs& args, hipStream_t st) {
@@ -686,10 +554,9 @@ void launch_wgrad(WgArgs& args, hipStream_t st) {
     for (int si = 0; si < args.p[i].nslot; ++si)
       if (args.p[i].slot[si].qoff + args.p[i].slot[si].rank > 16) narrow = false;
   }
-  const char* ve = getenv("MIFT_WGRAD_V");  // A/B knob, read per launch: 1 = the v1 kernel
-  const bool v1 = ve != nullptr && atoi(ve) == 1;
-  const int nqt = (narrow && !v1) ? 1 : 2;
+  const int nqt = narrow ? 1 : 2;
   at::Tensor ws;
+  args.flags = nullptr;
   if (mift_deterministic()) {
     ws = at::empty({(int64_t)blk * nqt * 16 * 64}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
     args.ws = ws.data_ptr<float>();
@@ -698,25 +565,16 @@ void launch_wgrad(WgArgs& args, hipStream_t st) {
       args.p[i].tile0 = tiles;
       tiles += args.p[i].P / 64;
     }
-    // MIFT_WGRAD_FIN=1 (opt-in): the last chunk block of every column tile reduces in place instead of
-    // a second launch.  Round 3's form gave every block an agent-scope release (L2 write-back of its
-    // XCD): step 5.09 -> 6.74 ms (profiles/r3/step_ab_wgrad_finisher_rejected.jsonl); round 4 stores the
-    // slabs write-through and counts arrivals relaxed (common.h mift_group_arrival).
-    const char* fe = getenv("MIFT_WGRAD_FIN");
-    const bool fin = !v1 && fe && atoi(fe) == 1;
-    args.flags = fin ? wg_flags(tiles) : nullptr;
-    if (v1) lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
-    else if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
+    if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
     else lora_wgrad2_kernel<T, 2><<<blk, 256, 0, st>>>(args);
-    if (fin) return;
+    // (an in-launch slab reduction by each column tile's last chunk block was measured cost-neutral at
+    // best, round 4, profiles/r4/step_ab_wgrad_fin_write_through.jsonl, and removed in round 6)
     if (nqt == 1) lora_wgrad_reduce_kernel<1><<<tiles, 256, 0, st>>>(args);
     else lora_wgrad_reduce_kernel<2><<<tiles, 256, 0, st>>>(args);
     return;
   }
-  args.flags = nullptr;
   args.ws = nullptr;
-  if (v1) lora_wgrad_kernel<T><<<blk, 256, 0, st>>>(args);
-  else if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
+  if (narrow) lora_wgrad2_kernel<T, 1><<<blk, 256, 0, st>>>(args);
   else lora_wgrad2_kernel<T, 2><<<blk, 256, 0, st>>>(args);
 }
 }  // namespace

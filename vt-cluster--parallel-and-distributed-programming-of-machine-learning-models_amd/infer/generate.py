@@ -142,9 +142,9 @@ class _DecodeGraph:
 
     def __init__(self, model, B, S0, max_new, padded, pad, eos, fill, H, hd, dtype, dev):
         self.key = (B, S0, max_new, padded, pad, eos, fill)
-        # the graph holds raw pointers to the model's weights: keep the model alive so its id() (part of
-        # the cache key) cannot be reused by a rebuilt model whose weights live elsewhere
-        self.model = model
+        # the graph holds raw pointers to the model's weights; the cache holds the model only weakly
+        # (a dead or different model under the same id() evicts the entry in _decode_graph)
+        self.model_ref = weakref.ref(model)
         L = len(model.blocks())
         self.cache = KVCache(L, B, H, S0 + max_new, hd, dtype, dev)
         self.B, self.S0, self.H, self.hd, self.fill, self.pad, self.eos = B, S0, H, hd, fill, pad, eos
@@ -316,9 +316,13 @@ def _arena_version(model):
 
 
 def _decode_graph(model, key_args):
-    # keyed by the adapter weights' version too: a graph captured before an optimizer step is not reused
-    # after it (its packs are rebuilt per replay, but the key keeps the contract explicit and cheap)
-    key = (id(model), _arena_version(model)) + tuple(key_args[:10])
+    # Not keyed by the adapter version: every replay rebuilds the LoRA operand packs inside the graph
+    # (captured pack launches read the live fp32 arena), so a graph stays valid across optimizer steps
+    # and one entry per (model, shape) is kept — the version key made every generate() after a step pay
+    # an eager call + a new capture and kept up to 4 stale KV caches / pools resident.
+    key = (id(model),) + tuple(key_args[:10])
+    for k in [k for k, g in _GRAPHS.items() if g.model_ref() is None or (k[0] == id(model) and g.model_ref() is not model)]:
+        _GRAPHS.pop(k)  # dead model, or a new model that reuses a dead one's id()
     g = _GRAPHS.get(key)
     if g is None:
         if len(_GRAPHS) >= 4:

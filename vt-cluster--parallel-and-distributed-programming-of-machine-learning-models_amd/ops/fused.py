@@ -471,10 +471,16 @@ def _infer_ln_gemm(x, ln, lin):
 def _ln_fold(ln, lin, w):
     """(wf, c1, c2) of LayerNorm(x; γ, β)·wᵀ + bias with the LN folded into the weights: wf = γ∘w rounded
     to w's dtype, c1 = Σ_k wf[:, k] and c2 = w·β + bias in fp32 (K.gemm_ln_fold).  Cached on the linear,
-    keyed by the storage and version counters of every operand (rebuilt after any in-place update)."""
+    keyed by the storage and version counters of the SOURCE parameters (each member linear's weight and
+    bias, the LN's): ``w`` itself may be a derived cached tensor (a transpose / concatenation) whose
+    rebuilt copy can land at the same address with version 0, so keying on it could reuse stale folds
+    (ADVICE r5)."""
     b = lin.bias
-    key = (w.data_ptr(), w._version, ln.weight.data_ptr(), ln.weight._version, ln.bias.data_ptr(), ln.bias._version,
-           None if b is None else (b.data_ptr(), b._version))
+    members = getattr(lin, "lins", None) or [lin]
+    src = tuple((m.weight.data_ptr(), m.weight._version) if getattr(m, "weight", None) is not None else None
+                for m in members)
+    key = (src, w.data_ptr(), w._version, w.shape, ln.weight.data_ptr(), ln.weight._version, ln.bias.data_ptr(),
+           ln.bias._version, None if b is None else (b.data_ptr(), b._version))
     c = getattr(lin, "_mift_lnfold", None)
     if c is None or c[0] != key:
         g, beta = ln.weight.detach().float(), ln.bias.detach().float()

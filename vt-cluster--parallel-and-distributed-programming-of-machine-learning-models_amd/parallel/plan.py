@@ -79,8 +79,20 @@ def _divisors(n):
     return [d for d in range(1, n + 1) if n % d == 0]
 
 
+GRAPH_OP_OVERHEAD_S = 20e-6   # per chunk-micro-batch (fwd + bwd) when the stage graphs replay
+EAGER_OP_OVERHEAD_S = 60e-6   # ... when the schedule runs eagerly (host-issued launches)
+
+
+def stage_graphs_expected(recompute=False, fused=True):
+    """Whether the PP engine will replay per-slot stage hipGraphs (the trainer's
+    ``_fused_graphable("pipeline")``: fused GPU LoRA path, no recompute, MIFT_GRAPH not off)."""
+    import os
+    mode = os.environ.get("MIFT_GRAPH", "auto")
+    return bool(fused) and not recompute and mode not in ("off", "0", "false", "")
+
+
 def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_bytes=2, name=None, virtual=1,
-            op_overhead_s=None):
+            op_overhead_s=None, graphed=True):
     """Predicted step time and per-GPU efficiency of an S-stage pipeline at micro-batch ``mb``
     (``virtual`` > 1: interleaved schedule with that many model chunks per rank).
 
@@ -106,7 +118,7 @@ def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_
     rank_units = [sum(units[c * stages + r] for c in range(v)) for r in range(stages)]
     seq_ms = cost_per_seq_ms(name, mb, measured)          # whole model, dp1, per sequence
     u = seq_ms * 1e-3 * mb / (L + head_layers)             # s per layer-equivalent per micro-batch
-    ovh = op_overhead_s if op_overhead_s is not None else 20e-6
+    ovh = op_overhead_s if op_overhead_s is not None else (GRAPH_OP_OVERHEAD_S if graphed else EAGER_OP_OVERHEAD_S)
     hop = mb * seq * d * dtype_bytes / LINK_BW + LINK_LAT
     step = (m * max(rank_units) + (stages - 1) * max(units)) * u + m * v * ovh + 2 * (nvs - 1) / stages * hop
     best_dp1 = min(cost_per_seq_ms(name, x, measured) for x in _divisors(per_replica))
@@ -137,13 +149,16 @@ def graph_slots(stages, micro_batches, virtual, rank=0):
 
 
 def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=288 * 10 ** 9,
-                       hbm_frac=0.85, measured=None, name=None, candidates=None, virtual=1, graph_sets=None):
+                       hbm_frac=0.85, measured=None, name=None, candidates=None, virtual=1, graph_sets=None,
+                       graphed=None):
     """The feasible micro-batch (divisor of ``per_replica``) with the shortest predicted step.
     ``virtual``: model chunks per rank (int), or "auto" to choose among 1, 2, 4, ... as well.
     Memory: rank 0's live activations at the end of the eager warm-up, or ``graph_sets`` captured
     slot sets of stage graphs (``MIFT_PP_GRAPH_SETS``, default 2: the epoch's ragged last step keeps
     its own set), whichever is larger (the eager step's cached blocks are released before a capture)."""
     import os
+    if graphed is None:
+        graphed = stage_graphs_expected()
     if graph_sets is None:
         graph_sets = int(os.environ.get("MIFT_PP_GRAPH_SETS", "2"))
     L = cfg.num_layers() if hasattr(cfg, "num_layers") else cfg.num_hidden_layers
@@ -168,13 +183,19 @@ def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=2
             held = max(inflight, graph_sets * graph_slots(stages, m, v)) if stages > 1 else inflight
             need = held * mb * seq * per_tok      # rank 0's live activations (eager warm-up or graph slots)
             p = predict(cfg, seq, per_replica, stages, mb, measured=measured, dtype_bytes=dtype_bytes, name=name,
-                        virtual=v)
+                        virtual=v, graphed=graphed)
             p["act_gib"] = round(need / GiB, 2)
             p["graph_slot_sets"] = graph_sets
             p["fits"] = need <= budget
             table.append(p)
             if p["fits"] and (best is None or p["step_ms"] < best["step_ms"] - 1e-9):
                 best = p
+    if not table:
+        if vs != [1]:  # every (mb, V > 1) pair was excluded by the m % stages rule: plain 1F1B instead
+            return choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes, hbm_bytes, hbm_frac, measured,
+                                      name, candidates, 1, graph_sets, graphed)
+        raise ValueError(f"choose_micro_batch: no micro-batch candidate for per_replica={per_replica}, "
+                         f"stages={stages}, virtual={virtual}")
     if best is None:
         best = table[0]
     out = dict(best)
