@@ -53,3 +53,17 @@ def test_debug_kernel_build_compiles(tmp_path):
     cmd = [B.HIPCC, "-x", "hip", "-c", src, "-o", str(tmp_path / "e.o")] + B._common_flags() + ["-DMIFT_DEBUG=1"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
+
+
+def test_pinned_accumulator_check_parses_resource_remarks():
+    """build.py refuses a GEMM object whose 4-wave 256x256 tile has fewer than 256 AGPRs (its
+    accumulators copied between register files around every MFMA: the round-6 79 -> 514 ms slip)."""
+    from mift import build as B
+    k10 = "_ZN12_GLOBAL__N_114gemm_nt_kernelIDF16_Li256ELi256ELi2ELi2ELi1ELb0ELi0ELi64EEEvPKT_"
+    k8 = "_ZN12_GLOBAL__N_114gemm_nt_kernelIDF16_Li256ELi256ELi4ELi2ELi3ELb0ELi0ELi64EEEvPKT_"
+    rem = lambda k, a: (f"gemm_impl.h:1:1: remark: {k}: Function Name: {k} [-Rpass-analysis=kernel-resource-usage]\n"
+                        f"gemm_impl.h:1:1: remark: {k}:     VGPRs: 256 [-Rpass-analysis=kernel-resource-usage]\n"
+                        f"gemm_impl.h:1:1: remark: {k}:     AGPRs: {a} [-Rpass-analysis=kernel-resource-usage]\n")
+    assert B.check_pinned_accumulators(rem(k10, 256) + rem(k8, 0)) == []
+    bad = B.check_pinned_accumulators(rem(k8, 0) + rem(k10, 65))
+    assert len(bad) == 1 and bad[0][1] == 65

@@ -814,3 +814,29 @@ def test_mask_positions_matches_torch(S):
     pos, kv = K_.mask_positions(mask)
     assert torch.equal(pos, opt_positions(mask))
     assert torch.equal(kv, mask.sum(1, dtype=torch.int32))
+
+
+@pytest.mark.parametrize("tile", [7, 8, 9, 10])
+@pytest.mark.parametrize("epi", ["fwd", "dgrad_masked"])
+def test_gemm_hoisted_dropout_hash_bit_identical(tile, epi, monkeypatch):
+    """The epilogues' dropout-mask hashes from the hoisted high-word mix (MIFT_EPI_HOIST=1, default:
+    residual-dropout keep8 in the staged phase 2, masked K-extension keep4 in phase 1) draw exactly the
+    masks of the per-call form (MIFT_EPI_HOIST=0)."""
+    C = _C()
+    torch.manual_seed(9)
+    M, N, K = 1536, 3072 if tile == 9 else 2304, 768
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    a2 = torch.randn(M, 32, device="cuda", dtype=torch.bfloat16)
+    b2 = torch.randn(N, 32, device="cuda", dtype=torch.bfloat16) * 0.1
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    aux = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    outs = []
+    for h in ("0", "1"):
+        monkeypatch.setenv("MIFT_EPI_HOIST", h)
+        if epi == "fwd":
+            outs.append(_gnt(C, a, b, bias, a2, b2, 0, None, res, 0.1, 5, False, 1.0, None, tile, None, None, 0.0, 0)[0])
+        else:
+            outs.append(_gnt(C, a, b, None, a2, b2, 4, aux, None, 0.0, 0, False, 1.0, None, tile, None, None, 0.05, 77)[0])
+    assert torch.equal(outs[0], outs[1])

@@ -86,6 +86,26 @@ def _common_flags():
     return flags
 
 
+_TILE10 = "Li256ELi256ELi2ELi2E"  # gemm_nt_kernel<T, 256, 256, 2, 2, ...>: the 4-wave mainloop4 tile
+
+
+def check_pinned_accumulators(remarks):
+    """The 4-wave 256x256 tile keeps its 256 fp32 accumulators in AGPRs through inline-asm MFMAs
+    (`"+a"` operands, gemm_impl.h mfma_acc).  Under register pressure the allocator may keep them in
+    VGPRs instead and copy them into AGPRs around every asm statement: bit-identical output, but the
+    OPT-2.7B step went 79 -> 514 ms when one extra live value in the epilogue did that (round 6).
+    Returns the offending kernels' (name, AGPR count) from hipcc's kernel-resource-usage remarks."""
+    bad, cur = [], None
+    for line in remarks.splitlines():
+        if "Function Name:" in line:
+            cur = line.split("Function Name:", 1)[1].split()[0]
+        elif cur and "gemm_nt_kernel" in cur and _TILE10 in cur and "AGPRs:" in line:
+            n = int(line.split("AGPRs:", 1)[1].split()[0])
+            if n < 256:
+                bad.append((cur[:80], n))
+    return bad
+
+
 def _compile(src, flags, force, verbose, build_dir=BUILD_DIR):
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_") if src.startswith(CSRC) else os.path.basename(src)
     obj = os.path.join(build_dir, rel + ".o")
@@ -103,11 +123,22 @@ def _compile(src, flags, force, verbose, build_dir=BUILD_DIR):
     cmd = [HIPCC, "-c", src, "-o", obj] + flags
     if src.endswith(".hip"):
         cmd = [HIPCC, "-x", "hip", "-c", src, "-o", obj] + flags
+    gemm = os.path.basename(src).startswith("gemm")
+    if gemm:
+        cmd.append("-Rpass-analysis=kernel-resource-usage")
     if verbose:
         print(" ".join(cmd), flush=True)
     p = subprocess.run(cmd, capture_output=True, text=True)
     if p.returncode != 0:
         raise RuntimeError(f"compile failed: {src}\n{p.stdout}\n{p.stderr}")
+    if gemm:
+        bad = check_pinned_accumulators(p.stderr)
+        if bad:
+            os.remove(obj)
+            raise RuntimeError(f"{src}: the 4-wave 256x256 GEMM tile lost its AGPR-pinned accumulators "
+                               f"(needs 256 AGPRs; copies around every MFMA made it ~6x slower): {bad}")
+        p = subprocess.CompletedProcess(p.args, 0, p.stdout, "\n".join(
+            l for l in p.stderr.splitlines() if "kernel-resource-usage" not in l))
     with open(stamp, "w") as fh:
         fh.write(digest)
     return obj, True, p.stderr

@@ -143,6 +143,7 @@ struct EpiArgs {
   // started (prologue done), [2] main loop done, [3] C tile in LDS, [4] exit; s_memrealtime at [6] / [7]
   long long* stamps;
   int staged;     // interior tiles: feature-staged epilogue phase 2 (MIFT_EPI_STAGED, default 1)
+  int hoist;      // dropout-mask hashes with the hoisted high-word mix (output < 2^33 elements; MIFT_EPI_HOIST)
 };
 
 // Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
@@ -800,6 +801,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
     // compile-time split so the common unmasked body stays a short straight-line block (the 4-wave
     // tile unrolls 64 fragments: the masked hash inlined into each cost it 36k cycles of I-cache-bound
     // code per tile, tools/gemm_stamps.py)
+    const uint32_t ehm = mift_hmix(ep.ext_seed, 0);
     auto phase1 = [&](auto maskedc) {
       constexpr bool MASKED = decltype(maskedc)::value;
   #pragma unroll
@@ -823,7 +825,13 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
           if (MASKED || (NSTAGE != 1 && ext_masked)) {
             float4_ xt = mfma16<T>(bf2[j], af2[i], float4_{0.f, 0.f, 0.f, 0.f});
             bool kp[4];
-            mift_keep4(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col, ep.ext_thr, kp);
+            // pair index < 2^32 (host-checked): one hoisted high-word mix, no branches.  Not on the
+            // 4-wave tile: the extra live value there pushed its 256 pinned accumulators out of the
+            // AGPRs (256 -> 65, copies around every MFMA: OPT step 79 -> 514 ms; build.py checks)
+            if (NSTAGE != 1 && ep.hoist)
+              mift_keep4_hm(ep.ext_seed, ehm, (uint64_t)(m0 + row) * N + n0 + col, ep.ext_thr, kp);
+            else
+              mift_keep4(ep.ext_seed, (uint64_t)(m0 + row) * N + n0 + col, ep.ext_thr, kp);
   #pragma unroll
             for (int e = 0; e < 4; ++e) z[e] += kp[e] ? xt[e] * ep.ext_inv_keep : 0.f;
           }
@@ -1019,6 +1027,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
       const T* auxp = reinterpret_cast<const T*>(ep.aux);
       const T* resp = reinterpret_cast<const T*>(ep.residual);
       const bool sb_bwd = ep.act == ACT_RELU_BWD && ep.aux == nullptr && ep.sbits != nullptr;
+      const uint32_t dhm = mift_hmix(ep.seed, 0);
       for (int g0 = 0; g0 < ITER; g0 += G) {
         int row[G], c8[G];
         size_t off[G];
@@ -1105,7 +1114,17 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
   #pragma unroll
           for (int k = 0; k < G; ++k) {
             bool kp[8];
-            mift_keep8(ep.seed, (uint64_t)(m0 + row[k]) * N + n0 + c8[k], ep.thr, kp);
+            if (NSTAGE != 1 && ep.hoist) {  // the 4 pairs' hashes from the hoisted high-word mix
+              const uint32_t lo = (uint32_t)(((uint64_t)(m0 + row[k]) * N + n0 + c8[k]) >> 1);
+  #pragma unroll
+              for (int e = 0; e < 8; e += 2) {
+                const uint32_t h = mift_hash_lo(ep.seed, dhm, lo + (e >> 1));
+                kp[e] = (h & 0xFFFFu) >= ep.thr;
+                kp[e + 1] = (h >> 16) >= ep.thr;
+              }
+            } else {
+              mift_keep8(ep.seed, (uint64_t)(m0 + row[k]) * N + n0 + c8[k], ep.thr, kp);
+            }
   #pragma unroll
             for (int e = 0; e < 8; ++e) z[k][e] = kp[e] ? z[k][e] * ep.inv_keep : 0.f;
           }
@@ -2827,6 +2846,8 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
   {
     const char* e = getenv("MIFT_EPI_STAGED");  // read per call (A/B)
     ep.staged = e ? atoi(e) : 1;
+    const char* h = getenv("MIFT_EPI_HOIST");   // read per call (A/B); needs M·N < 2^33
+    ep.hoist = (h ? atoi(h) : 1) && (uint64_t)M * N < (1ull << 33);
   }
   ep.sbits = nullptr;
   if (sbits) {  // ReLU sign bits: written (act = relu) or read in place of aux (act = relu backward)
