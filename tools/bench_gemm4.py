@@ -97,12 +97,17 @@ def check(C, tiles):
     return ok
 
 
-def bench(C, tiles, results):
+def bench(C, tiles, results, only=None):
     shapes = [(f"{n}@M{M}", M, N, K, torch.float16) for M in (6144, 24576) for n, N, K in OPT_LAYER]
     shapes += [("lm_head.fwd.dgpt", 8192, 50304, 768, torch.bfloat16),
                ("lm_head.dgrad.dgpt", 8192, 768, 50304, torch.bfloat16),
                ("square4k", 4096, 4096, 4096, torch.bfloat16),
-               ("opt.lm_head.fwd@M6144", 6144, 50304, 2560, torch.float16)]
+               ("opt.lm_head.fwd@M6144", 6144, 50304, 2560, torch.float16),
+               # split-K proxy of the LM-head dgrad: its 8 K-chunks of 6288 as 8x the rows (same tiles,
+               # same per-tile K length, same FLOPs; no partial-slab reduction)
+               ("lm_head.dgrad.dgpt.split8_proxy", 8 * 8192, 768, 6272, torch.bfloat16)]
+    if only:
+        shapes = [s for s in shapes if any(o in s[0] for o in only.split(","))]
     wins = 0
     for name, M, N, K, dt in shapes:
         a, b, _ = operands(M, N, K, dt, scale=False)
@@ -161,6 +166,7 @@ def main():
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--tiles", default="8,10")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, help="comma-separated name filters for the timing shapes")
     a = ap.parse_args()
     assert mift.kernels_available(), mift._ext.error()
     import mift._C as C
@@ -173,7 +179,7 @@ def main():
     if a.sweep:
         sweep(C, tiles, results)
     else:
-        bench(C, tiles, results)
+        bench(C, tiles, results, a.only)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(results, f, indent=1)

@@ -21,13 +21,17 @@ import mift  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="8,10")
+    ap.add_argument("--shapes", default="opt", help="opt | dgpt (the K = 768 distilgpt2 block GEMMs, bf16)")
     a = ap.parse_args()
     import mift._C as C
-    shapes = [(6144, 7680, 2560), (6144, 2560, 2560), (6144, 2560, 640)]
+    if a.shapes == "dgpt":
+        shapes, dt = [(8192, 3072, 768), (8192, 2304, 768), (8192, 768, 3072), (8192, 768, 768)], torch.bfloat16
+    else:
+        shapes, dt = [(6144, 7680, 2560), (6144, 2560, 2560), (6144, 2560, 640)], torch.float16
     for M, N, K in shapes:
-        x = torch.randn(M, K, device="cuda", dtype=torch.float16)
-        w = torch.randn(N, K, device="cuda", dtype=torch.float16)
-        nblk = ((M + 255) // 256) * ((N + 255) // 256)
+        x = torch.randn(M, K, device="cuda", dtype=dt)
+        w = torch.randn(N, K, device="cuda", dtype=dt)
+        nblk = ((M + 63) // 64) * ((N + 63) // 64)  # >= the block count of any tile
         for tile in [int(t) for t in a.tiles.split(",")]:
             for store in (1, 0):
                 os.environ["MIFT_LM_DBG"] = "0" if store else "1"
@@ -37,9 +41,9 @@ def main():
                     C.gemm_nt(x, w, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, tile, None, None, 0.0, 0)
                 torch.cuda.synchronize()
                 C.gemm_set_stamps(None)
-                s = buf.view(nblk, 8).cpu().tolist()
+                s = [b for b in buf.view(nblk, 8).cpu().tolist() if b[0] != 0]  # launched blocks only
                 med = lambda v: statistics.median(v)  # noqa: E731
-                row = {"shape": f"{M}x{N}x{K}", "tile": tile, "c_store": bool(store), "blocks": nblk}
+                row = {"shape": f"{M}x{N}x{K}", "tile": tile, "c_store": bool(store), "blocks": len(s)}
                 if tile == 10:
                     row["prologue_cyc"] = med([b[1] - b[0] for b in s])
                     row["loop_cyc"] = med([b[2] - b[1] for b in s])
