@@ -1,5 +1,6 @@
 """LM-head dgrad (EPI 2) with and without its per-column-group accumulator rescale (MIFT_LM_DBG bit 3:
-timing only, wrong numbers), distilgpt2 shape, interleaved rounds in one process."""
+timing only, wrong numbers) and over the split-K count (MIFT_LM_SPLIT), distilgpt2 and OPT-2.7B shapes,
+interleaved rounds in one process."""
 import json
 import os
 import statistics
@@ -35,13 +36,17 @@ def main():
         E, stats, lse, loss, zlab = K.lmhead_fwd(a, w, lab, V)[:5]
         g = torch.ones(1, device="cuda")
         res = {}
+        arms = {"default": {}, "no_rescale": {"MIFT_LM_DBG": "8"}}
+        for sp in (4, 6, 7, 8, 10, 12):
+            arms[f"split{sp}"] = {"MIFT_LM_SPLIT": str(sp)}
         for _ in range(3):
-            for dbg in ("0", "8"):
-                os.environ["MIFT_LM_DBG"] = dbg
-                res.setdefault(dbg, []).append(timeit(lambda: K.lmhead_dgrad(E, wt, w, lab, V, stats, lse, g)))
-        os.environ.pop("MIFT_LM_DBG", None)
-        print(json.dumps({"M": M, "d": d, "V": V, "dgrad_us": round(min(res["0"]) * 1e3, 1),
-                          "dgrad_no_rescale_us": round(min(res["8"]) * 1e3, 1)}), flush=True)
+            for name, env in arms.items():
+                os.environ.update(env)
+                res.setdefault(name, []).append(timeit(lambda: K.lmhead_dgrad(E, wt, w, lab, V, stats, lse, g)))
+                for k in env:
+                    os.environ.pop(k, None)
+        print(json.dumps({"M": M, "d": d, "V": V, **{k + "_us": round(min(v) * 1e3, 1) for k, v in res.items()}}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -203,7 +203,8 @@ MIFT_HD float apply_act(int act, float z, float aux) {
 
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;  // bytes per LDS row (128)
-constexpr int LM_GW = 24;     // LM-head dgrad: groups (forward column tiles) per LDS window of tile maxima
+constexpr int LM_GW = 25;     // LM-head dgrad: groups (forward column tiles) per LDS window of tile maxima (25: the
+                              // distilgpt2 chunks of 25 groups take one window, OPT's of 50 two)
 
 // s_waitcnt vmcnt(n) with a compile-time n (0..63)
 template <int N>
@@ -1377,13 +1378,24 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
     for (int w0 = g0; w0 < g1; w0 += LM_GW) {
       const int w1 = min(g1, w0 + LM_GW), nw = w1 - w0;
       __syncthreads();  // the previous window's readers are done
-      // one 32-lane half-wave per row (nw <= 32 lanes active): each half writes one row's nw words
-      // -> distinct banks (ds_write_b32 groups are the two half-waves), and reads a contiguous run
-      // of the row's stats from global; the odd stride keeps the fragment-row reads conflict-free
-      static_assert(LM_GW <= 32, "window fill: one half-wave per row");
-      for (int r = tid >> 5; r < BM; r += NT / 32) {
-        const int g = tid & 31;
-        if (g < nw) ms[r * cstride + g] = lm.stats[(size_t)min(m0 + r, M - 1) * lm.ntn + w0 + g].x;
+      // each thread requests PB window entries before their LDS writes (a per-row loop waited for
+      // each row's load in turn: 16 round trips per window; all 13 at once spill the accumulators),
+      // element i = (row i / LM_GW, group i % LM_GW); the odd stride keeps the fragment-row reads
+      // conflict-free
+      constexpr int PER = (BM * LM_GW + NT - 1) / NT, PB = 5;
+#pragma unroll 1
+      for (int u0 = 0; u0 < PER; u0 += PB) {
+        float wv[PB];
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+          const int i = tid + (u0 + u) * NT, r = i / LM_GW, g = i % LM_GW;
+          wv[u] = (i < BM * LM_GW && g < nw) ? lm.stats[(size_t)min(m0 + r, M - 1) * lm.ntn + w0 + g].x : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+          const int i = tid + (u0 + u) * NT;
+          if (i < BM * LM_GW) ms[(i / LM_GW) * cstride + i % LM_GW] = wv[u];
+        }
       }
       __syncthreads();
       mainloop8(w0 * GK, min(nk_all, w1 * GK), [&](int kt) {
