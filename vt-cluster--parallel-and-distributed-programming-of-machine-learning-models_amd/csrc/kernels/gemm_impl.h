@@ -2470,17 +2470,31 @@ __global__ __launch_bounds__(256) void lmhead_lse_kernel(const float2* __restric
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6) + k * rstride;
     if (row >= M) break;  // wave-uniform
     const float2* st = stats + (size_t)row * ntn;
-    float m = -INFINITY;
-    for (int j = lane; j < ntn; j += 64) m = fmaxf(m, st[j].x);
-    m = wave_max(m);
-    float s = 0.f;
-    for (int j = lane; j < ntn; j += 64) s += st[j].y * __expf(st[j].x - m);
+    // the row's target and label logit requested with its stats (not after the reduction)
+    const int64_t lab = lm_label(labels, row, shift, ignore);
+    const float zl = zlab[row];  // written for rows with a target, read only for those
+    float m = -INFINITY, s = 0.f;
+    constexpr int JL = 4;  // a row's stats in registers when ntn <= 256: ONE memory round trip per row
+    if (ntn <= 64 * JL) {  // (the loops below waited for every load in turn)
+      float2 v[JL];
+#pragma unroll
+      for (int u = 0; u < JL; ++u) v[u] = lane + 64 * u < ntn ? st[lane + 64 * u] : make_float2(-INFINITY, 0.f);
+#pragma unroll
+      for (int u = 0; u < JL; ++u) m = fmaxf(m, v[u].x);
+      m = wave_max(m);
+#pragma unroll
+      for (int u = 0; u < JL; ++u)  // same per-lane order as the loop form: bit-identical
+        if (lane + 64 * u < ntn) s += v[u].y * __expf(v[u].x - m);
+    } else {
+      for (int j = lane; j < ntn; j += 64) m = fmaxf(m, st[j].x);
+      m = wave_max(m);
+      for (int j = lane; j < ntn; j += 64) s += st[j].y * __expf(st[j].x - m);
+    }
     s = wave_sum(s);
     if (lane == 0) {
       const float l = m + __logf(s);
       lse[row] = l;
-      const int64_t lab = lm_label(labels, row, shift, ignore);
-      const float lrow = (lab >= 0 && lab < V) ? l - zlab[row] : 0.f;
+      const float lrow = (lab >= 0 && lab < V) ? l - zl : 0.f;
       loss[row] = lrow;
       lsum += lrow;
     }
