@@ -73,7 +73,8 @@ def parse_args(argv=None):
     ap.add_argument("--virtual_stages", dest="virtual", default=None,
                     help="interleaved 1F1B model chunks per pipeline rank; 'auto' (PP default): chosen with the "
                          "micro-batch by mift.parallel.plan")
-    ap.add_argument("--partition", default="balanced", choices=["uniform", "balanced"])
+    ap.add_argument("--partition", default=None, choices=["uniform", "balanced", "halves"],
+                    help="pipeline split (default: halves for OPT — half-layer units —, else balanced)")
     ap.add_argument("--zero", type=int, default=0)
     ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "fp32"],
                     help="default bf16 (GPT-2) / fp16 (OPT)")
@@ -186,7 +187,8 @@ def main():
         cands = None if a.micro_batch == "auto" else [int(a.micro_batch)]
         plan = choose_micro_batch(mcfg, a.seq_len, per_rank, a.pp, dtype_bytes=2, name=a.model, candidates=cands,
                                   virtual="auto" if a.virtual == "auto" else int(a.virtual),
-                                  graphed=stage_graphs_expected(fused=a.impl == "fused" and a.device != "cpu"))
+                                  graphed=stage_graphs_expected(fused=a.impl == "fused" and a.device != "cpu"),
+                                  partition=a.partition or ("halves" if is_opt else "balanced"))
         a.micro_batch, a.virtual = str(plan["micro_batch"]), str(plan["virtual"])
     V = int(a.virtual)
     ctx = D.init(pp=a.pp, verbose=False, sanity=True, virtual=V)
@@ -210,8 +212,10 @@ def main():
     split = None
     kw = {}
     if ctx.pp > 1:
-        from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_chunks
-        split = partition_layers(mcfg.num_layers(), ctx.pp * V, a.partition, head_cost_layers(mcfg), ranks=ctx.pp)
+        from mift.parallel.pipeline import attn_cost_fraction, head_cost_layers, partition_layers, stage_chunks
+        part = a.partition or ("halves" if is_opt else "balanced")
+        split = partition_layers(mcfg.num_layers(), ctx.pp * V, part, head_cost_layers(mcfg), ranks=ctx.pp,
+                                 attn_frac=attn_cost_fraction(mcfg))
         chunks = stage_chunks(split, ctx.pp, V, ctx.pp_rank)
         kw = dict(layer_range=chunks if V > 1 else chunks[0], has_embed=ctx.is_first_stage,
                   has_head=ctx.is_last_stage)

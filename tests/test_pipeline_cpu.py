@@ -110,6 +110,40 @@ def test_pipeline_4_stages_balanced(single_drop):
     _close_runs(r[0], single_drop)
 
 
+def test_pipeline_half_layer_stages_match_single(single_drop):
+    """Half-layer partition units (``partition_layers(..., "halves")``): stage boundaries that split a
+    decoder layer between its attention and MLP sub-blocks (2 stages: [2.5, 1.5] layers; 4 stages:
+    [1.5, 1, 1, 0.5]) reproduce the single-process run with dropout on, and the adapters gathered from
+    the stages are exactly the model's (each half layer holds only its own sub-block's adapters)."""
+    r = harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, partition="halves")
+    assert r[0]["split"] == [2.5, 1.5]
+    _close_runs(r[0], single_drop)
+    r = harness.run(_worker, 4, pp=4, accum=4, dropout=0.1, partition="halves")
+    assert r[0]["split"] == [1.5, 1.0, 1.0, 0.5]
+    _close_runs(r[0], single_drop)
+
+
+def test_interleaved_half_layer_chunks_match_single(single_drop):
+    r = harness.run(_worker, 2, pp=2, dropout=0.1, virtual=2, partition="halves")
+    assert any(x != int(x) for x in r[0]["split"]), r[0]["split"]
+    _close_runs(r[0], single_drop)
+
+
+def test_half_layer_partition_balances_opt_configs():
+    """BASELINE configs 3 / 5: whole-layer units leave the slowest rank 1.07 / 1.21 of the mean
+    (profiles/r5/stage_time_config{3,5}.json); half-layer units bring the cost model to <= 1.03 / 1.08."""
+    from mift.models.opt import OPTConfig
+    from mift.parallel.pipeline import attn_cost_fraction, head_cost_layers, split_rank_costs
+    for name, S, V, whole, half in (("opt-2.7b", 4, 4, 1.07, 1.03), ("opt-6.7b", 8, 2, 1.21, 1.08)):
+        cfg = OPTConfig.preset(name)
+        h, n, af = head_cost_layers(cfg), cfg.num_hidden_layers, attn_cost_fraction(cfg)
+        for method, bound in (("balanced", whole + 0.01), ("halves", half)):
+            split = partition_layers(n, S * V, method, h, ranks=S, attn_frac=af)
+            assert sum(split) == n and all(x > 0 and 2 * x == int(2 * x) for x in split)
+            c = split_rank_costs(split, S, h, attn_frac=af)
+            assert max(c) / (sum(c) / S) <= bound, (name, method, split, c)
+
+
 def test_dp_x_pp_matches_single(single):
     r = harness.run(_worker, 4, pp=2, accum=4)
     _close_runs(r[0], single)

@@ -12,7 +12,7 @@ GPU_ENV = {"MIFT_DEVICE": "cuda", "MIFT_BACKEND": "gloo"}
 
 
 def _worker(rank, world, pp=1, graph=False, steps=3, mb=2, accum=6, p2p="link", max_grad_norm=1.0,
-            consistency_every=0, zero=0, virtual=1):
+            consistency_every=0, zero=0, virtual=1, partition="uniform"):
     import os
     os.environ["MIFT_PP_P2P"] = p2p
     from mift import lora as L
@@ -25,7 +25,7 @@ def _worker(rank, world, pp=1, graph=False, steps=3, mb=2, accum=6, p2p="link", 
 
     ctx = D.init(pp=pp, verbose=False, sanity=True, virtual=virtual)
     cfg = OPTConfig.preset("opt-tiny")
-    split = partition_layers(cfg.num_hidden_layers, ctx.pp * virtual, "uniform", head_cost_layers(cfg))
+    split = partition_layers(cfg.num_hidden_layers, ctx.pp * virtual, partition, head_cost_layers(cfg))
     lr_ = stage_layer_range(split, ctx.pp_rank) if virtual == 1 else stage_chunks(split, ctx.pp, virtual, ctx.pp_rank)
     model = build_causal_lm("opt-tiny", dtype=torch.float16, device=ctx.device, seed=3,
                             layer_range=lr_, has_embed=ctx.is_first_stage, has_head=ctx.is_last_stage)
@@ -75,6 +75,18 @@ def test_pipeline_graphs_match_eager_and_single(single, pp):
         assert eager[r]["stats"]["replays"] == 0
     _close(eager[0], single, 2e-3)
     _close(graph[0], eager[0], 1e-3)
+
+
+@pytest.mark.parametrize("pp,virtual", [(2, 1), (4, 1), (2, 2)])
+def test_half_layer_stages_on_gpu(single, pp, virtual):
+    """Half-layer pipeline boundaries on the fused kernels (a stage ending after a layer's attention
+    sub-block hands the residual stream to the next one, which runs that layer's MLP sub-block without
+    the fused out_proj dropout-backward handoff): eager == single, stage graphs == eager."""
+    r = harness.run(_worker, pp, env=GPU_ENV, timeout=240, pp=pp, virtual=virtual, partition="halves")
+    _close(r[0], single, 2e-3)
+    g = harness.run(_worker, pp, env=GPU_ENV, timeout=240, pp=pp, virtual=virtual, partition="halves", graph=True)
+    assert g[0]["stats"]["replays"] > 0
+    _close(g[0], r[0], 1e-3)
 
 
 def test_interleaved_pipeline_on_gpu(single):

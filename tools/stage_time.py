@@ -47,20 +47,21 @@ class LocalP2P:
         return Pending([], out, [], None)
 
 
-def run_rank(model_name, S, V, s, mb, seq, per_replica, steps, warmup, precision="fp16"):
+def run_rank(model_name, S, V, s, mb, seq, per_replica, steps, warmup, precision="fp16", partition="balanced"):
     import torch
     from mift import lora as L
     from mift.data import MicroBatcher, synthetic_openwebtext
     from mift.models import build_causal_lm
     from mift.models.opt import OPTConfig
     from mift.parallel import dist as D
-    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_chunks
+    from mift.parallel.pipeline import attn_cost_fraction, head_cost_layers, partition_layers, stage_chunks
     from mift.train.trainer import TrainConfig, Trainer
 
     ctx = D.init(pp=1, verbose=False, sanity=False)  # world 1; the grid below is simulated
     ctx.pp, ctx.pp_rank, ctx.pp_ranks, ctx.pp_virtual = S, s, list(range(S)), V
     cfg = OPTConfig.preset(model_name)
-    split = partition_layers(cfg.num_hidden_layers, S * V, "balanced", head_cost_layers(cfg), ranks=S)
+    split = partition_layers(cfg.num_hidden_layers, S * V, partition, head_cost_layers(cfg), ranks=S,
+                             attn_frac=attn_cost_fraction(cfg))
     chunks = stage_chunks(split, S, V, s)
     dtype = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}[precision]
     model = build_causal_lm(model_name, dtype=dtype, device=ctx.device, seed=0,
@@ -93,7 +94,7 @@ def run_rank(model_name, S, V, s, mb, seq, per_replica, steps, warmup, precision
         tr.train_step(all_steps[i])
     sync()
     dt = (time.perf_counter() - t0) / steps
-    out = {"rank": s, "chunks": [list(c) for c in chunks], "layers": sum(b - a for a, b in chunks),
+    out = {"rank": s, "chunks": [list(c) for c in chunks], "layers": sum(b - a for a, b in chunks), "partition": partition,
            "embed": s == 0, "head": s == S - 1, "micro_batch": mb, "micro_batches": acc,
            "ms_per_step": round(dt * 1e3, 2), "ms_per_micro_batch": round(dt * 1e3 / acc, 3),
            "replays": eng.stats.get("replays", 0), "split": split,
@@ -116,6 +117,7 @@ def main():
     ap.add_argument("--model", default=None, help="override the config's model (e.g. opt-tiny for a CPU check)")
     ap.add_argument("--precision", default="fp16")
     ap.add_argument("--pp", type=int, default=None, help="override the config's stage count")
+    ap.add_argument("--partition", default="balanced", choices=["uniform", "balanced", "halves"])
     ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.child is not None:
@@ -130,14 +132,14 @@ def main():
     cfg = OPTConfig.preset(name)
     plan = choose_micro_batch(cfg, a.seq_len, a.per_replica, S, name=name,
                               candidates=[a.micro_batch] if a.micro_batch else None,
-                              virtual=a.virtual if a.virtual else "auto")
+                              virtual=a.virtual if a.virtual else "auto", partition=a.partition)
     mb, V = plan["micro_batch"], plan["virtual"]
-    pred = predict(cfg, a.seq_len, a.per_replica, S, mb, name=name, virtual=V)
+    pred = predict(cfg, a.seq_len, a.per_replica, S, mb, name=name, virtual=V, partition=a.partition)
     ranks = [int(r) for r in a.ranks.split(",")] if a.ranks else list(range(S))
     rows = []
     for s in ranks:
         kw = dict(model_name=name, S=S, V=V, s=s, mb=mb, seq=a.seq_len, per_replica=a.per_replica,
-                  steps=a.steps, warmup=a.warmup, precision=a.precision)
+                  steps=a.steps, warmup=a.warmup, precision=a.precision, partition=a.partition)
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", json.dumps(kw)],
                            capture_output=True, text=True, cwd=ROOT)
         res = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")]
@@ -149,10 +151,12 @@ def main():
         print(json.dumps(r), flush=True)
     worst = max(r["ms_per_micro_batch"] for r in rows)
     summary = {"config": a.config, "model": name, "stages": S, "dp": dp, "virtual": V, "micro_batch": mb,
+               "partition": a.partition,
                "pred_stage_ms": pred["stage_ms"], "meas_stage_ms": worst,
                "meas_over_pred": round(worst / pred["stage_ms"], 3), "pred_step_ms": pred["step_ms"],
                "per_rank_ms_per_micro_batch": [r["ms_per_micro_batch"] for r in rows],
-               "bubble_free_step_ms": round(worst * rows[0]["micro_batches"], 2)}
+               "bubble_free_step_ms": round(worst * rows[0]["micro_batches"], 2),
+               "slowest_over_mean": round(worst / (sum(r["ms_per_micro_batch"] for r in rows) / len(rows)), 3)}
     print("SUMMARY " + json.dumps(summary), flush=True)
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)

@@ -39,7 +39,7 @@ from ..data.tokenizer import load_tokenizer
 from ..models import build_causal_lm
 from ..obs.timing import PhaseLogger, p2_loss_line
 from ..parallel import dist as D
-from ..parallel.pipeline import head_cost_layers, partition_layers, stage_chunks, stage_layer_range
+from ..parallel.pipeline import attn_cost_fraction, head_cost_layers, partition_layers, stage_chunks, stage_layer_range
 from ..train.trainer import TrainConfig, Trainer
 
 
@@ -61,8 +61,10 @@ def build_argparser():
                     help="interleaved 1F1B: model chunks per pipeline rank, or 'auto' (chosen with the micro-batch "
                          "by the planner); default $PIPELINE_VIRTUAL_STAGES, mift.virtual_stages, else 'auto' when "
                          "the micro-batch is planned and 1 otherwise")
-    ap.add_argument("--partition", choices=["uniform", "balanced"], default=None,
-                    help="layer split (default: mift.pp_partition / pipeline.partition_method, else balanced)")
+    ap.add_argument("--partition", choices=["uniform", "balanced", "halves"], default=None,
+                    help="layer split (default: mift.pp_partition / pipeline.partition_method, else balanced; "
+                         "halves: half-layer units, a stage boundary may split a decoder layer between its "
+                         "attention and MLP sub-blocks)")
     ap.add_argument("--precision", choices=["fp16", "bf16", "fp32"], default=None)
     ap.add_argument("--micro_batch", default=None,
                     help="GPU micro-batch: regroups batch*accum sequences per step into micro-batches of this "
@@ -126,7 +128,8 @@ def plan_micro_batch(args, ds, stages, world, gpu):
         rec = bool(getattr(args, "gradient_checkpointing", False)) or bool(getattr(ds, "activation_checkpointing", False))
         plan = choose_micro_batch(cfg, args.seq_len, per_step, stages, dtype_bytes=2, name=args.model_name,
                                   candidates=None if mbsel == "auto" else [mbsel or base_mb],
-                                  virtual=vsel, graphed=stage_graphs_expected(recompute=rec))
+                                  virtual=vsel, graphed=stage_graphs_expected(recompute=rec),
+                                  partition=args.partition or ds.pp_partition)
         mbsel, vsel = plan["micro_batch"], plan["virtual"]
     elif mbsel == "auto":
         mbsel = 0
@@ -182,7 +185,8 @@ def main(argv=None):
     cfg = OPTConfig.preset(args.model_name)
     N = cfg.num_hidden_layers
     V = ctx.pp_virtual
-    split = partition_layers(N, ctx.pp * V, args.partition or ds.pp_partition, head_cost_layers(cfg), ranks=ctx.pp)
+    split = partition_layers(N, ctx.pp * V, args.partition or ds.pp_partition, head_cost_layers(cfg), ranks=ctx.pp,
+                             attn_frac=attn_cost_fraction(cfg))
     mine = stage_chunks(split, ctx.pp, V, ctx.pp_rank)  # V == 1: one contiguous range
     lo, hi = mine[0][0], mine[-1][1]
     model = build_causal_lm(args.model_name, dtype=dtype, device=ctx.device, seed=args.seed,

@@ -16,7 +16,7 @@ Reference: P2 loads a DeepSpeed JSON (``--ds_cfg``,
   (288 GB of HBM per MI355X holds weights, optimizer state and activations);
 * ``mift`` section (MI355X-specific, defaults sized for one process per GPU over xGMI):
   ``kernels`` (HIP kernels on/off), ``graph`` (hipGraph replay: auto/on/off), ``lmhead``
-  (fused | blas), ``bucket_mb`` (DP all-reduce bucket), ``pp_partition`` (uniform | balanced),
+  (fused | blas), ``bucket_mb`` (DP all-reduce bucket), ``pp_partition`` (uniform | balanced | halves: half-layer units),
   ``pp_schedule`` (1f1b), ``micro_batch`` (GPU micro-batch regrouping: an int, or "auto" = the
   pipeline planner ``mift.parallel.plan.choose_micro_batch``), ``virtual_stages`` (interleaved 1F1B
   chunks per pipeline rank: an int, or "auto" = chosen with the micro-batch), ``side_stream``
@@ -152,7 +152,7 @@ class MiftConfig:
         c.consistency_every = int(m.get("consistency_every", 0))
         c.max_inflight_steps = int(m.get("max_inflight_steps", 2))
         for name, val, ok in [("graph", c.graph, ("auto", "on", "off")), ("lmhead", c.lmhead, ("fused", "blas")),
-                              ("pp_partition", c.pp_partition, ("uniform", "balanced")),
+                              ("pp_partition", c.pp_partition, ("uniform", "balanced", "halves")),
                               ("pp_schedule", c.pp_schedule, ("1f1b",))]:
             if val not in ok:
                 raise ValueError(f"mift.{name} must be one of {ok}, got {val!r}")

@@ -9,7 +9,7 @@ the pipeline engine and the generator treat them alike:
     build only one pipeline stage's weights: SURVEY §6 — the reference OOMs
     because every rank materialises the whole fp32 model first);
   * interleaved pipeline stages (``parallel/pipeline.py``, virtual stages): ``layer_range`` may
-    be a LIST of (lo, hi) chunks; the pipeline engine selects one with ``active_chunk`` before a
+    be a LIST of (lo, hi) chunks (OPT: bounds on half layers, ``normalize_chunks``); the pipeline engine selects one with ``active_chunk`` before a
     forward, which then runs only that chunk's blocks, the embedding only on the first chunk of the
     first stage and the head only on the last chunk of the last stage;
   * ``seed`` / ``micro_step``: counter-based dropout seeds, so a block
@@ -25,20 +25,35 @@ from ..ops.dispatch import use_kernels
 from .layers import dropout_seed, seed_for
 
 
-def normalize_chunks(layer_range, n_layers):
+def _on_grid(x, step):
+    return abs(x / step - round(x / step)) < 1e-9
+
+
+def normalize_chunks(layer_range, n_layers, halves=False):
     """``layer_range``: None (all layers), (lo, hi), or [(lo, hi), ...] (interleaved chunks)
-    -> (span (lo, hi), chunk list, per-layer membership)"""
+    -> (span (lo, hi), chunk list, per-layer membership).  ``halves`` (OPT): bounds may fall on half
+    layers — unit 2i is layer i's attention sub-block (LN, q/k/v, attention, out_proj + residual),
+    unit 2i + 1 its MLP sub-block — so a pipeline boundary can split a decoder layer at its residual
+    stream (``chunk_parts``)."""
     if layer_range is None:
         chunks = [(0, n_layers)]
     elif isinstance(layer_range[0], (tuple, list)):
         chunks = [tuple(c) for c in layer_range]
     else:
         chunks = [tuple(layer_range)]
+    step = 0.5 if halves else 1
     for lo, hi in chunks:
-        if not (0 <= lo < hi <= n_layers):
-            raise ValueError(f"bad layer chunk {(lo, hi)} for {n_layers} layers")
-    member = [any(lo <= i < hi for lo, hi in chunks) for i in range(n_layers)]
+        if not (0 <= lo < hi <= n_layers) or not (_on_grid(lo, step) and _on_grid(hi, step)):
+            raise ValueError(f"bad layer chunk {(lo, hi)} for {n_layers} layers"
+                             + ("" if halves else " (whole layers only for this model)"))
+    member = [any(lo < i + 1 and i < hi for lo, hi in chunks) for i in range(n_layers)]
     return (min(c[0] for c in chunks), max(c[1] for c in chunks)), chunks, member
+
+
+def chunk_parts(chunks, i):
+    """(attention sub-block, MLP sub-block) of layer ``i`` inside any of ``chunks``."""
+    return (any(lo <= i and i + 0.5 <= hi for lo, hi in chunks),
+            any(lo <= i + 0.5 and i + 1 <= hi for lo, hi in chunks))
 
 
 class CausalLMBase(nn.Module):
@@ -50,7 +65,12 @@ class CausalLMBase(nn.Module):
         if self.active_chunk is None:
             return bl
         lo, hi = self.chunk_ranges[self.active_chunk]
-        return [b for b in bl if lo <= b.idx < hi]
+        return [b for b in bl if lo < b.idx + 1 and b.idx < hi]
+
+    def block_parts(self, blk):
+        """(attention, MLP) sub-blocks of ``blk`` this forward runs (half-layer pipeline chunks)."""
+        chunks = self.chunk_ranges if self.active_chunk is None else [self.chunk_ranges[self.active_chunk]]
+        return chunk_parts(chunks, blk.idx)
 
     @property
     def embed_here(self):

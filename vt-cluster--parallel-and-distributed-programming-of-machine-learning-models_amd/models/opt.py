@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import reference as ref
-from .base import CausalLMBase, normalize_chunks, ref_lm_loss, shift_labels
+from .base import CausalLMBase, chunk_parts, normalize_chunks, ref_lm_loss, shift_labels
 from .layers import ConcatLinear, Embedding, LayerNorm, Linear, dropout_seed, init_normal_, padded_vocab, seed_for
 
 
@@ -106,76 +106,88 @@ class OPTAttention(nn.Module):
 class OPTDecoderLayer(nn.Module):
     SITES = ["attn", "attn_out", "mlp_out", "lora_attn", "lora_proj", "lora_fc1", "lora_fc2"]
 
-    def __init__(self, cfg: OPTConfig, idx: int, dtype=None, device=None):
+    def __init__(self, cfg: OPTConfig, idx: int, dtype=None, device=None, parts=(True, True)):
+        """``parts`` = (attention sub-block, MLP sub-block) this stage holds: a half-layer pipeline
+        boundary (models/base.py ``normalize_chunks``) builds only its side's weights and adapters."""
         super().__init__()
-        self.idx, self.cfg = idx, cfg
+        self.idx, self.cfg, self.parts = idx, cfg, tuple(parts)
         d = cfg.hidden_size
-        self.self_attn = OPTAttention(cfg, dtype, device)
-        self.self_attn_layer_norm = LayerNorm(d, cfg.layer_norm_eps, dtype=dtype, device=device)
-        self.fc1 = Linear(d, cfg.ffn_dim, bias=cfg.enable_bias, dtype=dtype, device=device)
-        self.fc2 = Linear(cfg.ffn_dim, d, bias=cfg.enable_bias, dtype=dtype, device=device)
-        self.final_layer_norm = LayerNorm(d, cfg.layer_norm_eps, dtype=dtype, device=device)
+        if parts[0]:
+            self.self_attn = OPTAttention(cfg, dtype, device)
+            self.self_attn_layer_norm = LayerNorm(d, cfg.layer_norm_eps, dtype=dtype, device=device)
+        if parts[1]:
+            self.fc1 = Linear(d, cfg.ffn_dim, bias=cfg.enable_bias, dtype=dtype, device=device)
+            self.fc2 = Linear(cfg.ffn_dim, d, bias=cfg.enable_bias, dtype=dtype, device=device)
+            self.final_layer_norm = LayerNorm(d, cfg.layer_norm_eps, dtype=dtype, device=device)
 
     def site_seeds(self, base, step):
         s = 100 + 10 * self.idx
         return {k: dropout_seed(base, step, s + i) for i, k in enumerate(self.SITES)}
 
-    def forward_ref(self, h, seeds, training, key_valid=None, attn=None):
+    def forward_ref(self, h, seeds, training, key_valid=None, attn=None, parts=(True, True)):
         """h: [B, S, d] (reference path).  One LoRA-dropout seed for q/k/v (see MultiAdapterOps).
-        ``attn(qkv [B,S,3d]) -> o [B,S,d]`` overrides the attention (KV-cache decode)."""
+        ``attn(qkv [B,S,3d]) -> o [B,S,d]`` overrides the attention (KV-cache decode).  ``parts``:
+        the sub-blocks to run (a half-layer pipeline stage runs one)."""
         cfg = self.cfg
         B, S, d = h.shape
-        H, hd = self.self_attn.n_head, self.self_attn.head_dim
-        at = self.self_attn
-        a = self.self_attn_layer_norm(h)
-        sl = seeds["lora_attn"]
-        q, k, v = at.q_proj(a, sl), at.k_proj(a, sl), at.v_proj(a, sl)
-        if attn is not None:
-            o = attn(torch.cat([q, k, v], -1))
-        else:
-            q = q.view(B, S, H, hd).transpose(1, 2)
-            k = k.view(B, S, H, hd).transpose(1, 2)
-            v = v.view(B, S, H, hd).transpose(1, 2)
-            o = ref.attention(q, k, v, causal=True, key_padding=key_valid, scale=hd ** -0.5,
-                              dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"])
-            o = o.transpose(1, 2).reshape(B, S, d)
-        y = at.out_proj(o, seeds["lora_proj"])
-        if training and cfg.dropout > 0:
-            y = ref.dropout(y, cfg.dropout, seeds["attn_out"])
-        h = h + y
-        a2 = self.final_layer_norm(h)
-        f = torch.relu(self.fc1(a2, seeds["lora_fc1"]))
-        y2 = self.fc2(f, seeds["lora_fc2"])
-        if training and cfg.dropout > 0:
-            y2 = ref.dropout(y2, cfg.dropout, seeds["mlp_out"])
-        return h + y2
+        if parts[0]:
+            H, hd = self.self_attn.n_head, self.self_attn.head_dim
+            at = self.self_attn
+            a = self.self_attn_layer_norm(h)
+            sl = seeds["lora_attn"]
+            q, k, v = at.q_proj(a, sl), at.k_proj(a, sl), at.v_proj(a, sl)
+            if attn is not None:
+                o = attn(torch.cat([q, k, v], -1))
+            else:
+                q = q.view(B, S, H, hd).transpose(1, 2)
+                k = k.view(B, S, H, hd).transpose(1, 2)
+                v = v.view(B, S, H, hd).transpose(1, 2)
+                o = ref.attention(q, k, v, causal=True, key_padding=key_valid, scale=hd ** -0.5,
+                                  dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"])
+                o = o.transpose(1, 2).reshape(B, S, d)
+            y = at.out_proj(o, seeds["lora_proj"])
+            if training and cfg.dropout > 0:
+                y = ref.dropout(y, cfg.dropout, seeds["attn_out"])
+            h = h + y
+        if parts[1]:
+            a2 = self.final_layer_norm(h)
+            f = torch.relu(self.fc1(a2, seeds["lora_fc1"]))
+            y2 = self.fc2(f, seeds["lora_fc2"])
+            if training and cfg.dropout > 0:
+                y2 = ref.dropout(y2, cfg.dropout, seeds["mlp_out"])
+            h = h + y2
+        return h
 
-    def forward_fused(self, h, seeds, training, kv_len=None, attn=None):
+    def forward_fused(self, h, seeds, training, kv_len=None, attn=None, parts=(True, True)):
         from ..ops import fused as F
         from ..ops.attention import causal_attention
         cfg = self.cfg
         B, S, d = h.shape
-        at = self.self_attn
-        H, hd = at.n_head, at.head_dim
-        link = None
-        if at.qkv.fusable():
-            link = F.ResidualLink()  # residual grad of h enters the LN backward (no separate add)
-            qkv = F.ln_linear(h, self.self_attn_layer_norm, at.qkv, seeds["lora_attn"], training, link=link)
-        else:  # adapters too wide for one shared K-extension: three projections
-            qkv = torch.cat([F.ln_linear(h, self.self_attn_layer_norm, l, seeds["lora_attn"], training)
-                             for l in (at.q_proj, at.k_proj, at.v_proj)], -1)
-        if attn is not None:
-            o = attn(qkv)
-        else:
-            o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5,
-                                 dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"],
-                                 kv_len=kv_len)
-        # the MLP's LN backward also runs out_proj's residual-dropout backward + dT (one row pass)
-        hand = F.GradHandoff() if training and torch.is_grad_enabled() else None
-        h = F.linear_residual(o, h, at.out_proj, cfg.dropout, seeds["attn_out"], seeds["lora_proj"], training,
-                              link=link, handoff=hand)
-        return F.mlp(h, self.final_layer_norm, self.fc1, self.fc2, act=2, p=cfg.dropout, seed=seeds["mlp_out"],
-                     seed_l1=seeds["lora_fc1"], seed_l2=seeds["lora_fc2"], training=training, handoff=hand)
+        # the MLP's LN backward also runs out_proj's residual-dropout backward + dT (one row pass) when
+        # both sub-blocks run here; a half-layer stage boundary between them takes the separate passes
+        hand = F.GradHandoff() if training and torch.is_grad_enabled() and parts[0] and parts[1] else None
+        if parts[0]:
+            at = self.self_attn
+            H, hd = at.n_head, at.head_dim
+            link = None
+            if at.qkv.fusable():
+                link = F.ResidualLink()  # residual grad of h enters the LN backward (no separate add)
+                qkv = F.ln_linear(h, self.self_attn_layer_norm, at.qkv, seeds["lora_attn"], training, link=link)
+            else:  # adapters too wide for one shared K-extension: three projections
+                qkv = torch.cat([F.ln_linear(h, self.self_attn_layer_norm, l, seeds["lora_attn"], training)
+                                 for l in (at.q_proj, at.k_proj, at.v_proj)], -1)
+            if attn is not None:
+                o = attn(qkv)
+            else:
+                o = causal_attention(qkv, B, S, H, hd, scale=hd ** -0.5,
+                                     dropout_p=cfg.attention_dropout if training else 0.0, seed=seeds["attn"],
+                                     kv_len=kv_len)
+            h = F.linear_residual(o, h, at.out_proj, cfg.dropout, seeds["attn_out"], seeds["lora_proj"], training,
+                                  link=link, handoff=hand)
+        if parts[1]:
+            h = F.mlp(h, self.final_layer_norm, self.fc1, self.fc2, act=2, p=cfg.dropout, seed=seeds["mlp_out"],
+                      seed_l1=seeds["lora_fc1"], seed_l2=seeds["lora_fc2"], training=training, handoff=hand)
+        return h
 
 
 class OPTLearnedPositionalEmbedding(Embedding):
@@ -202,7 +214,7 @@ class OPTForCausalLM(CausalLMBase):
         self.config = cfg
         self.dtype_ = dtype
         n = cfg.num_hidden_layers
-        self.layer_range, self.chunk_ranges, member = normalize_chunks(layer_range, n)
+        self.layer_range, self.chunk_ranges, member = normalize_chunks(layer_range, n, halves=True)
         self.has_embed, self.has_head = has_embed, has_head
         d = cfg.hidden_size
         self.model = nn.Module()
@@ -212,7 +224,8 @@ class OPTForCausalLM(CausalLMBase):
         if has_embed:
             dec.embed_positions = OPTLearnedPositionalEmbedding(cfg.max_position_embeddings, d, dtype, device)
         dec.layers = nn.ModuleList(
-            [OPTDecoderLayer(cfg, i, dtype, device) if member[i] else nn.Identity() for i in range(n)])
+            [OPTDecoderLayer(cfg, i, dtype, device, chunk_parts(self.chunk_ranges, i)) if member[i] else nn.Identity()
+             for i in range(n)])
         if has_head:
             dec.final_layer_norm = LayerNorm(d, cfg.layer_norm_eps, dtype=dtype, device=device)
         self._init_runtime(padded_vocab(cfg.vocab_size))
@@ -260,11 +273,12 @@ class OPTForCausalLM(CausalLMBase):
         h = self.embed_ref(input_ids, attention_mask) if self.embed_here else hidden_states
         for blk in self.blocks():
             seeds = blk.site_seeds(self.seed, self.micro_step)
+            parts = self.block_parts(blk)
             if self.recompute and self.training and torch.is_grad_enabled():
-                h = torch.utils.checkpoint.checkpoint(blk.forward_ref, h, seeds, self.training, key_valid,
-                                                      use_reentrant=False)
+                h = torch.utils.checkpoint.checkpoint(blk.forward_ref, h, seeds, self.training, key_valid, None,
+                                                      parts, use_reentrant=False)
             else:
-                h = blk.forward_ref(h, seeds, self.training, key_valid)
+                h = blk.forward_ref(h, seeds, self.training, key_valid, parts=parts)
         if not self.head_here:
             return {"hidden_states": h}
         loss, logits = self.head_ref(h, labels, reduction, ignore_index)
@@ -293,11 +307,12 @@ class OPTForCausalLM(CausalLMBase):
             h = hidden_states
         for blk in self.blocks():
             seeds = blk.site_seeds(self.seed, self.micro_step)
+            parts = self.block_parts(blk)
             if self.recompute and training and torch.is_grad_enabled():
-                h = torch.utils.checkpoint.checkpoint(blk.forward_fused, h, seeds, training, kv_len,
+                h = torch.utils.checkpoint.checkpoint(blk.forward_fused, h, seeds, training, kv_len, None, parts,
                                                       use_reentrant=False)
             else:
-                h = blk.forward_fused(h, seeds, training, kv_len)
+                h = blk.forward_fused(h, seeds, training, kv_len, parts=parts)
         if not self.head_here:
             return {"hidden_states": h}
         w_nk, w_kn = self.lm_weight_padded(transposed=labels is not None and torch.is_grad_enabled())

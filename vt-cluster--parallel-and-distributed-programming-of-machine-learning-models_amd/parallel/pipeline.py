@@ -75,13 +75,45 @@ import torch
 from .comm import P2P
 
 
-def partition_layers(n_layers, n_stages, method="uniform", head_layers=0.0, embed_layers=0.0, ranks=None):
+# The attention sub-block's share of an OPT decoder layer's forward + backward time, measured per hidden
+# size (tools/half_layer_cost.py, fused path, LoRA on all six linears, seq 512: OPT-2.7B at micro-batch
+# 12 1.321 / 1.441 ms, OPT-6.7B at 6 1.415 / 1.858 ms: profiles/r6/half_layer_cost.jsonl); other sizes
+# interpolate; MIFT_PP_ATTN_FRAC overrides.
+ATTN_FRACTION = {2560: 0.478, 4096: 0.432}
+
+
+def attn_cost_fraction(cfg):
+    e = os.environ.get("MIFT_PP_ATTN_FRAC")
+    if e:
+        return float(e)
+    d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd", 2560)
+    xs = sorted(ATTN_FRACTION)
+    if d <= xs[0]:
+        return ATTN_FRACTION[xs[0]]
+    if d >= xs[-1]:
+        return ATTN_FRACTION[xs[-1]]
+    lo = max(x for x in xs if x <= d)
+    hi = min(x for x in xs if x >= d)
+    return ATTN_FRACTION[lo] if lo == hi else \
+        ATTN_FRACTION[lo] + (d - lo) / (hi - lo) * (ATTN_FRACTION[hi] - ATTN_FRACTION[lo])
+
+
+def partition_layers(n_layers, n_stages, method="uniform", head_layers=0.0, embed_layers=0.0, ranks=None,
+                     attn_frac=None):
     """-> list of per-stage layer counts (sum = n_layers).
 
     ``ranks`` (interleaved pipeline, n_stages = ranks x chunks): "balanced" then balances the per-RANK
     sums (virtual stage k runs on rank k % ranks): equal chunks, the last chunk (which carries the
     head) shortened by the head's layer-equivalents, the removed layers spread over the other
-    ranks' chunks from the front."""
+    ranks' chunks from the front.
+
+    "halves" (OPT): the partition unit is the half layer (attention sub-block, then MLP sub-block,
+    costing ``attn_frac`` (``attn_cost_fraction(cfg)``) and 1 − attn_frac of a layer), counts are multiples of 0.5 and the per-rank
+    costs (embedding on the first virtual stage, head on the last) are balanced: with whole layers
+    OPT-6.7B's 32 layers + a ~1-layer head over 8 ranks leave one rank 5 layers against a 4.13 mean
+    (slowest / mean 1.21, profiles/r5/stage_time_config5.json)."""
+    if method == "halves":
+        return _partition_halves(n_layers, n_stages, head_layers, embed_layers, ranks, attn_frac)
     if n_stages > n_layers:
         raise ValueError(f"{n_stages} stages > {n_layers} layers")
     if method == "uniform":
@@ -129,6 +161,81 @@ def _greedy(n, S, cap, head, embed):
         split.append(k)
         left -= k
     return split if left == 0 else None
+
+
+def _partition_halves(n_layers, n_stages, head, embed, ranks, attn_frac):
+    if attn_frac is None:
+        attn_frac = float(os.environ.get("MIFT_PP_ATTN_FRAC", 0.45))
+    nu = 2 * n_layers
+    if n_stages > nu:
+        raise ValueError(f"{n_stages} stages > {nu} half layers")
+    R = ranks if ranks and 1 < ranks < n_stages else n_stages
+    cum = [0.0]
+    for u in range(nu):
+        cum.append(cum[-1] + (attn_frac if u % 2 == 0 else 1.0 - attn_frac))
+
+    def rank_costs(b):
+        c = [0.0] * R
+        for k in range(n_stages):
+            c[k % R] += cum[b[k + 1]] - cum[b[k]] + (embed if k == 0 else 0.0) + (head if k == n_stages - 1 else 0.0)
+        return c
+
+    def score(b):  # slowest rank first, then the spread
+        c = rank_costs(b)
+        return (round(max(c), 9), round(sum(x * x for x in c), 9))
+
+    # boundaries at the cumulative cost targets (every virtual stage's share of the total, net of the
+    # embedding / head it carries), then a local search
+    total = cum[-1] + head + embed
+    b, target = [0], 0.0
+    for k in range(n_stages - 1):
+        target += total / n_stages - (embed if k == 0 else 0.0)
+        lo, hi = b[-1] + 1, nu - (n_stages - 1 - k)
+        j = min(range(lo, hi + 1), key=lambda x: abs(cum[x] - target))
+        b.append(j)
+    b.append(nu)
+    best = score(b)
+    for _ in range(4 * nu):  # moves: shift any run of consecutive boundaries by one unit
+        improved = False
+        for k1 in range(1, n_stages):
+            for k2 in range(k1, n_stages):
+                for dlt in (-1, 1):
+                    if not (b[k1 - 1] < b[k1] + dlt and b[k2] + dlt < b[k2 + 1]):
+                        continue
+                    cand = b[:k1] + [x + dlt for x in b[k1:k2 + 1]] + b[k2 + 1:]
+                    sc = score(cand)
+                    if sc < best:
+                        b, best, improved = cand, sc, True
+        if not improved:
+            break
+    return [(b[k + 1] - b[k]) / 2 for k in range(n_stages)]
+
+
+def split_chunk_costs(split, head=0.0, embed=0.0, attn_frac=None):
+    """Cost (layer-equivalents) of every virtual stage of ``split``: its layers, a half layer at either
+    end costed as its sub-block (``partition_layers(..., "halves")``), the embedding on the first and
+    the head on the last."""
+    if attn_frac is None:
+        attn_frac = float(os.environ.get("MIFT_PP_ATTN_FRAC", 0.45))
+    out, pos = [], 0.0
+    for k, n in enumerate(split):
+        lo, hi = pos, pos + n
+        c = hi - lo
+        if lo != int(lo):  # starts inside a layer: holds its MLP sub-block
+            c += (1.0 - attn_frac) - 0.5
+        if hi != int(hi):  # ends inside a layer: holds its attention sub-block
+            c += attn_frac - 0.5
+        out.append(c + (embed if k == 0 else 0.0) + (head if k == len(split) - 1 else 0.0))
+        pos = hi
+    return out
+
+
+def split_rank_costs(split, ranks, head=0.0, embed=0.0, attn_frac=None):
+    """Per-rank sums of ``split_chunk_costs`` (virtual stage k runs on rank k % ranks)."""
+    costs = [0.0] * ranks
+    for k, c in enumerate(split_chunk_costs(split, head, embed, attn_frac)):
+        costs[k % ranks] += c
+    return costs
 
 
 def stage_layer_range(split, stage):

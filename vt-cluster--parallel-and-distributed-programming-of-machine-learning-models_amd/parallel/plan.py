@@ -92,7 +92,7 @@ def stage_graphs_expected(recompute=False, fused=True):
 
 
 def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_bytes=2, name=None, virtual=1,
-            op_overhead_s=None, graphed=True):
+            op_overhead_s=None, graphed=True, partition="balanced"):
     """Predicted step time and per-GPU efficiency of an S-stage pipeline at micro-batch ``mb``
     (``virtual`` > 1: interleaved schedule with that many model chunks per rank).
 
@@ -101,10 +101,10 @@ def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_
     (or ``split``).  With u(mb) = dp1 time per layer-equivalent per micro-batch:
         step ≈ m·max_rank_units·u + (S − 1)·max_chunk_units·u + m·V·op_overhead + hops
     (the steady state runs at the slowest rank; warm-up and cool-down traverse the pipeline one
-    chunk at a time).  ``op_overhead``: fixed cost per chunk-micro-batch (fwd + bwd): p2p latency and
+    chunk at a time).  ``partition``: "balanced" (whole layers) or "halves" (half-layer units).  ``op_overhead``: fixed cost per chunk-micro-batch (fwd + bwd): p2p latency and
     host launches — 20 µs graph-replayed (both schedules replay per-slot stage graphs since round 5),
     60 µs eager."""
-    from .pipeline import partition_layers
+    from .pipeline import attn_cost_fraction, partition_layers, split_chunk_costs
     name = name or getattr(cfg, "name_or_path", None) or "opt-2.7b"
     L = cfg.num_layers() if hasattr(cfg, "num_layers") else cfg.num_hidden_layers
     d = getattr(cfg, "hidden_size", None) or getattr(cfg, "n_embd")
@@ -113,8 +113,8 @@ def predict(cfg, seq, per_replica, stages, mb, split=None, measured=None, dtype_
     nvs = stages * v
     head_layers = cfg.vocab_size / (12.0 * d)
     if split is None:
-        split = partition_layers(L, nvs, "balanced", head_layers, ranks=stages)
-    units = [n + (head_layers if k == nvs - 1 else 0.0) for k, n in enumerate(split)]
+        split = partition_layers(L, nvs, partition, head_layers, ranks=stages, attn_frac=attn_cost_fraction(cfg))
+    units = split_chunk_costs(split, head_layers, attn_frac=attn_cost_fraction(cfg))  # half-layer ends: sub-block
     rank_units = [sum(units[c * stages + r] for c in range(v)) for r in range(stages)]
     seq_ms = cost_per_seq_ms(name, mb, measured)          # whole model, dp1, per sequence
     u = seq_ms * 1e-3 * mb / (L + head_layers)             # s per layer-equivalent per micro-batch
@@ -150,7 +150,7 @@ def graph_slots(stages, micro_batches, virtual, rank=0):
 
 def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=288 * 10 ** 9,
                        hbm_frac=0.85, measured=None, name=None, candidates=None, virtual=1, graph_sets=None,
-                       graphed=None):
+                       graphed=None, partition="balanced"):
     """The feasible micro-batch (divisor of ``per_replica``) with the shortest predicted step.
     ``virtual``: model chunks per rank (int), or "auto" to choose among 1, 2, 4, ... as well.
     Memory: rank 0's live activations at the end of the eager warm-up, or ``graph_sets`` captured
@@ -183,7 +183,7 @@ def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=2
             held = max(inflight, graph_sets * graph_slots(stages, m, v)) if stages > 1 else inflight
             need = held * mb * seq * per_tok      # rank 0's live activations (eager warm-up or graph slots)
             p = predict(cfg, seq, per_replica, stages, mb, measured=measured, dtype_bytes=dtype_bytes, name=name,
-                        virtual=v, graphed=graphed)
+                        virtual=v, graphed=graphed, partition=partition)
             p["act_gib"] = round(need / GiB, 2)
             p["graph_slot_sets"] = graph_sets
             p["fits"] = need <= budget
@@ -193,7 +193,7 @@ def choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes=2, hbm_bytes=2
     if not table:
         if vs != [1]:  # every (mb, V > 1) pair was excluded by the m % stages rule: plain 1F1B instead
             return choose_micro_batch(cfg, seq, per_replica, stages, dtype_bytes, hbm_bytes, hbm_frac, measured,
-                                      name, candidates, 1, graph_sets, graphed)
+                                      name, candidates, 1, graph_sets, graphed, partition)
         raise ValueError(f"choose_micro_batch: no micro-batch candidate for per_replica={per_replica}, "
                          f"stages={stages}, virtual={virtual}")
     if best is None:
