@@ -94,7 +94,8 @@ def run_rank(model_name, S, V, s, mb, seq, per_replica, steps, warmup, precision
         tr.train_step(all_steps[i])
     sync()
     dt = (time.perf_counter() - t0) / steps
-    out = {"rank": s, "chunks": [list(c) for c in chunks], "layers": sum(b - a for a, b in chunks), "partition": partition,
+    out = {"rank": s, "chunks": [list(c) for c in chunks], "layers": sum(b - a for a, b in chunks),
+           "partition": partition,
            "embed": s == 0, "head": s == S - 1, "micro_batch": mb, "micro_batches": acc,
            "ms_per_step": round(dt * 1e3, 2), "ms_per_micro_batch": round(dt * 1e3 / acc, 3),
            "replays": eng.stats.get("replays", 0), "split": split,

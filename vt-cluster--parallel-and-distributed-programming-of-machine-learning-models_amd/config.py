@@ -16,7 +16,8 @@ Reference: P2 loads a DeepSpeed JSON (``--ds_cfg``,
   (288 GB of HBM per MI355X holds weights, optimizer state and activations);
 * ``mift`` section (MI355X-specific, defaults sized for one process per GPU over xGMI):
   ``kernels`` (HIP kernels on/off), ``graph`` (hipGraph replay: auto/on/off), ``lmhead``
-  (fused | blas), ``bucket_mb`` (DP all-reduce bucket), ``pp_partition`` (uniform | balanced | halves: half-layer units),
+  (fused | blas), ``bucket_mb`` (DP all-reduce bucket), ``pp_partition`` (uniform | balanced |
+  halves: half-layer units),
   ``pp_schedule`` (1f1b), ``micro_batch`` (GPU micro-batch regrouping: an int, or "auto" = the
   pipeline planner ``mift.parallel.plan.choose_micro_batch``), ``virtual_stages`` (interleaved 1F1B
   chunks per pipeline rank: an int, or "auto" = chosen with the micro-batch), ``side_stream``

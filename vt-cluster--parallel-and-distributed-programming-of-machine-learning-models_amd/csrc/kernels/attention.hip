@@ -518,7 +518,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
   const int klen = kv_len ? kv_len[b] : S;
   MIFT_ASSERT(klen >= 0 && klen <= S);
   const float c2 = scale * LOG2E;
-  const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
+  // hoisted-hash path: pair indices < 2^32 and (S even) every lane's element index i0 is even
+  const bool hze = (uint64_t)B * H * S * S < (1ull << 33) && S % 2 == 0;
   const uint32_t hm0 = mift_hmix(seed, 0);
 
   const int ng = g1;  // query groups [g0, g1) of this block (the whole head unless split)
@@ -587,7 +588,11 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
     for (int i = 0; i < G::NOT; ++i) o[i] = float4_{0.f, 0.f, 0.f, 0.f};
     const int kend = min(q0 + 16, klen);
     const int nkt = (kend + BKV - 1) / BKV;
-    for (int kt = 0; kt < nkt; ++kt) {
+    // one key tile; DIAG (compile-time) = the per-element causal / key-length mask.  Only a group's
+    // LAST key tile can reach past its queries or the key length, so the others run the mask-free
+    // instantiation (a runtime `diag` flag made hipcc emit one scalar branch per score element)
+    auto ktile = [&](const int kt, auto diagc) {
+      constexpr bool diag = decltype(diagc)::value;
       const int k0 = kt * BKV;
       float4_ st[4];
 #pragma unroll
@@ -597,14 +602,13 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
         for (int s = 0; s < G::NKS; ++s)
           st[t] = mfma16(ld_frag<T>(Ks + (k0 + t * 16 + qc) * G::RS + (4 * s + g) * 16), qf[s], st[t]);
       }
-      const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
       float tmax = -INFINITY;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = st[t][r] * c2;
-          if (diag) {
+          if constexpr (diag) {
             const int key = k0 + t * 16 + g * 4 + r;
             if (key > myq || key >= klen) v = -INFINITY;
           }
@@ -628,7 +632,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
         bool kp[4] = {true, true, true, true};
         if (thr != 0) {
           const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
-          if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
+          if (hze) mift_keep4_hm(seed, hm0, i0, thr, kp);  // block-uniform (i0 even when S is)
           else mift_keep4(seed, i0, thr, kp);
           const uint32_t nib = (uint32_t)kp[0] | ((uint32_t)kp[1] << 1) | ((uint32_t)kp[2] << 2) | ((uint32_t)kp[3] << 3);
           kbits[t >> 1] |= nib << ((t & 1) * 16 + g * 4);
@@ -673,7 +677,9 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
           const vec8<T> vf = tr_frag<T>(Vs, G::TRS, k0 + 32 * s2, i * 16, lane);
           o[i] = OT ? mfma16(vf, pf[s2], o[i]) : mfma16(pf[s2], vf, o[i]);
         }
-    }
+    };
+    for (int kt = 0; kt + 1 < nkt; ++kt) ktile(kt, std::false_type{});
+    if (nkt > 0) ktile(nkt - 1, std::true_type{});
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     const float inv_l = l > 0.f ? 1.f / l : 0.f;
@@ -1044,7 +1050,7 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
   const int klen = kv_len ? kv_len[b] : S;
   MIFT_ASSERT(klen >= 0 && klen <= S);
   const float c2 = scale * LOG2E;
-  const bool hz = (uint64_t)B * H * S * S < (1ull << 33);
+  const bool hze = (uint64_t)B * H * S * S < (1ull << 33) && S % 2 == 0;  // hoisted hash, even i0
   const uint32_t hm0 = mift_hmix(seed, 0);
   const int ng = g1;  // query groups [g0, g1) of this block (the whole head unless split)
   stage_rows<T, HD>(Ks, Kg, ld, S, SPB, tid, NT);
@@ -1091,10 +1097,11 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
     for (int i = 0; i < G::NOT; ++i) dq[i] = float4_{0.f, 0.f, 0.f, 0.f};
     const int kend = min(q0 + 16, klen);
     const int nkt = (kend + BKV - 1) / BKV;
-    for (int kt = 0; kt < nkt; ++kt) {
+    // compile-time causal / key-length mask: only the last key tile of a group needs it (as forward)
+    auto ktile = [&](const int kt, auto diagc) {
+      constexpr bool diag = decltype(diagc)::value;
       const int k0 = kt * BKV;
       vec8<T> dsf[2];
-      const bool diag = (k0 + BKV > q0) || (k0 + BKV > klen);
       uint2 kw = make_uint2(0u, 0u);
       if (mk) kw = *reinterpret_cast<const uint2*>((kt < 4 ? Ks : Vs) + (size_t)min(myq, S - 1) * G::RS + PADOFF + (kt & 3) * 8);
 #pragma unroll
@@ -1112,13 +1119,13 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
           for (int r = 0; r < 4; ++r) kp[r] = (e >> r) & 1u;
         } else if (thr != 0) {
           const uint64_t i0 = ((uint64_t)bh * S + myq) * S + k0 + t * 16 + g * 4;
-          if (hz && !(i0 & 1)) mift_keep4_hm(seed, hm0, i0, thr, kp);
+          if (hze) mift_keep4_hm(seed, hm0, i0, thr, kp);  // block-uniform (i0 even when S is)
           else mift_keep4(seed, i0, thr, kp);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float pr = fast_exp2(sa[r] * c2 - lse2);
-          if (diag) {
+          if constexpr (diag) {
             const int key = k0 + t * 16 + g * 4 + r;
             if (key > myq || key >= klen) pr = 0.f;
           }
@@ -1131,7 +1138,9 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
       for (int i = 0; i < G::NOT; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) dq[i] = mfma16(dsf[s2], tr_frag<T>(Ks, G::RS, k0 + 32 * s2, i * 16, lane), dq[i]);
-    }
+    };
+    for (int kt = 0; kt + 1 < nkt; ++kt) ktile(kt, std::false_type{});
+    if (nkt > 0) ktile(nkt - 1, std::true_type{});
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = q0 + g * 4 + r;

@@ -406,25 +406,34 @@ MIFT_HD void wg_reduce_tile(const WgArgs& args, const WgProb& pr, int pt) {
   const int ntp = pr.P / 64;
   const int nch = (pr.M + pr.rows - 1) / pr.rows;
   constexpr int SL = NQT * 16 * 64;
+  const size_t cstep = (size_t)ntp * SL;
+  const float* base = args.ws + (size_t)(pr.blk0 + pt) * SL;
+  // chunk slabs added strictly in chunk order (the deterministic result); the loads of all NQT
+  // column groups and CB chunks are issued together (the serial dependent-load chain was
+  // latency-bound, ~10 us per distilgpt2 layer; 8 chunks of one group at a time paid more trips)
+  constexpr int CB = 16 / NQT;  // chunk slabs per batch: 16 float4 loads in flight per thread
+  float4_ sum[NQT];
+#pragma unroll
+  for (int k = 0; k < NQT; ++k) sum[k] = float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int ch0 = 0; ch0 < nch; ch0 += CB) {
+    float4_ v[NQT][CB];
+#pragma unroll
+    for (int k = 0; k < NQT; ++k)
+#pragma unroll
+      for (int u = 0; u < CB; ++u)
+        v[k][u] = *reinterpret_cast<const float4_*>(base + (threadIdx.x + 256 * k) * 4 +
+                                                     (size_t)min(ch0 + u, nch - 1) * cstep);
+#pragma unroll
+    for (int k = 0; k < NQT; ++k)
+#pragma unroll
+      for (int u = 0; u < CB; ++u)
+        if (ch0 + u < nch) sum[k] += v[k][u];
+  }
 #pragma unroll
   for (int k = 0; k < NQT; ++k) {
     const int e = (threadIdx.x + 256 * k) * 4;  // slab element: [c][li][p]
     const int c = e / 1024, li = (e / 64) % 16, pl = e % 64;
-    // chunk slabs added strictly in chunk order (the deterministic result), their loads issued 8 at
-    // a time: the serial dependent-load chain was latency-bound (~10 us per distilgpt2 layer)
-    float4_ sum = float4_{0.f, 0.f, 0.f, 0.f};
-    const float* base = args.ws + (size_t)(pr.blk0 + pt) * SL + e;
-    const size_t cstep = (size_t)ntp * SL;
-#pragma unroll 1
-    for (int ch0 = 0; ch0 < nch; ch0 += 8) {
-      float4_ v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        v[u] = *reinterpret_cast<const float4_*>(base + (size_t)min(ch0 + u, nch - 1) * cstep);
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (ch0 + u < nch) sum += v[u];
-    }
     const int q = c * 16 + li;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -432,7 +441,7 @@ MIFT_HD void wg_reduce_tile(const WgArgs& args, const WgProb& pr, int pt) {
 #pragma unroll 1
       for (int si = 0; si < (pr.mode == 0 ? 1 : pr.nslot); ++si) {
         const int64_t o = wg_out_index(pr, pp, q, si);
-        if (o >= 0) args.out[o] += sum[r];
+        if (o >= 0) args.out[o] += sum[k][r];
       }
     }
   }
