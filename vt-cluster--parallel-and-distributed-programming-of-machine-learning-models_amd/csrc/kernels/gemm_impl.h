@@ -2399,7 +2399,8 @@ void dispatch_tile(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, cons
     }
     // one chip-wave of 128x96 tiles (1-2 per CU): the OPT micro-batch-4 shapes (M = 2048, N = 2560)
     // ran 20-30 % faster than on the 128x256 split-K / 128x128 tiles (fc2 fwd 167 -> 122 us, qkv dgrad
-    // 134 -> 94, out proj 50 -> 40; profiles/r4/bench_tiles_opt_pp_microbatch.json)
+    // 134 -> 94, out proj 50 -> 40; profiles/r4/bench_tiles_opt_pp_microbatch.json); the distilgpt2
+    // N = 768 GEMMs on the 8-wave 128x192 tile instead: step 4.634 -> 4.838 ms (profiles/r6)
     else if (t96 >= num_cus() && t96 <= 2L * num_cus()) tile = 7;
     else if (K >= 4096 && t128 >= 128) tile = 6;
     else if (N % 192 == 0 && (long)((M + 127) / 128) * (N / 192) >= 2L * num_cus()) tile = 9;
