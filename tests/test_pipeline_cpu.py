@@ -154,11 +154,13 @@ def test_zero1_matches_single(single):
     _close_runs(r[0], single)
 
 
-def test_pp_checkpoint_resume(tmp_path, single_drop):
-    """Stop after step 1 (checkpoint), resume in a fresh 2-stage job -> same result as uninterrupted."""
+@pytest.mark.parametrize("partition", ["uniform", "halves"])
+def test_pp_checkpoint_resume(tmp_path, single_drop, partition):
+    """Stop after step 1 (checkpoint), resume in a fresh 2-stage job -> same result as uninterrupted
+    (also with a stage boundary inside a decoder layer)."""
     d = str(tmp_path / "ck")
-    harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, steps=1, ckpt_dir=d)
-    r = harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, steps=2, ckpt_dir=d, resume="auto")
+    harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, steps=1, ckpt_dir=d, partition=partition)
+    r = harness.run(_worker, 2, pp=2, accum=4, dropout=0.1, steps=2, ckpt_dir=d, resume="auto", partition=partition)
     for k in single_drop["state"]:
         torch.testing.assert_close(r[0]["state"][k], single_drop["state"][k], atol=2e-5, rtol=1e-4)
 
