@@ -85,6 +85,38 @@ def test_stage_split_reconstructs_full_model():
     assert not any("embed" in k or "final_layer_norm.weight" == k.split("decoder.")[-1] for k in mid.state_dict())
 
 
+def test_half_layer_stages_reconstruct_full_model():
+    """Stage boundaries inside a decoder layer (between its attention and MLP sub-blocks): the stages
+    hold disjoint weight sets covering the full model exactly and chain to the full model's loss."""
+    cfg = _tiny()
+    full = OPTForCausalLM(cfg).init_weights(3).eval()
+    ids = torch.randint(3, cfg.vocab_size, (2, 12))
+    with torch.no_grad():
+        ref = full(input_ids=ids, labels=ids)["loss"]
+    s0 = OPTForCausalLM(cfg, layer_range=(0, 0.5), has_embed=True, has_head=False).eval()
+    s1 = OPTForCausalLM(cfg, layer_range=(0.5, 1.5), has_embed=False, has_head=False).eval()
+    s2 = OPTForCausalLM(cfg, layer_range=(1.5, 2), has_embed=False, has_head=True).eval()
+    fsd = full.state_dict()
+    layer_keys = set()
+    for s in (s0, s1, s2):
+        sd = s.state_dict()
+        assert set(sd) < set(fsd)
+        s.load_state_dict({k: fsd[k] for k in sd})
+        mine = {k for k in sd if ".layers." in k}
+        assert not (mine & layer_keys)  # no sub-block is held twice
+        layer_keys |= mine
+    assert layer_keys == {k for k in fsd if ".layers." in k}
+    assert not any("fc1" in k for k in s0.state_dict()) and not any("q_proj" in k for k in s2.state_dict())
+    with torch.no_grad():
+        h = s0(input_ids=ids)["hidden_states"]
+        h = s1(hidden_states=h)["hidden_states"]
+        loss = s2(hidden_states=h, labels=ids)["loss"]
+    torch.testing.assert_close(loss, ref)
+    from mift.models.gpt2 import GPT2Config, GPT2LMHeadModel
+    with pytest.raises(ValueError, match="whole layers"):
+        GPT2LMHeadModel(GPT2Config.preset("gpt2-tiny"), layer_range=(0, 0.5))
+
+
 def test_lora_counts_opt27b():
     cfg = OPTConfig.preset("facebook/opt-2.7b")
     with torch.device("meta"):
