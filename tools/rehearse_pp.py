@@ -30,7 +30,7 @@ def _worker(rank, world, model="facebook/opt-2.7b", pp=1, seq=512, mb=4, accum=2
     from mift.models import build_causal_lm
     from mift.models.opt import OPTConfig
     from mift.parallel import dist as D
-    from mift.parallel.pipeline import head_cost_layers, partition_layers, stage_chunks
+    from mift.parallel.pipeline import attn_cost_fraction, head_cost_layers, partition_layers, stage_chunks
     from mift.train.trainer import TrainConfig, Trainer
 
     ctx = D.init(pp=pp, verbose=False, sanity=True, virtual=virtual)
@@ -39,7 +39,8 @@ def _worker(rank, world, model="facebook/opt-2.7b", pp=1, seq=512, mb=4, accum=2
     split = None
     if ctx.pp > 1:
         V = ctx.pp_virtual
-        split = partition_layers(cfg.num_hidden_layers, ctx.pp * V, partition, head_cost_layers(cfg), ranks=ctx.pp)
+        split = partition_layers(cfg.num_hidden_layers, ctx.pp * V, partition, head_cost_layers(cfg), ranks=ctx.pp,
+                                 attn_frac=attn_cost_fraction(cfg))
         ch = stage_chunks(split, ctx.pp, V, ctx.pp_rank)
         kw = dict(layer_range=ch if V > 1 else ch[0], has_embed=ctx.is_first_stage, has_head=ctx.is_last_stage)
     m = build_causal_lm(model, dtype=torch.float16, device=ctx.device, seed=0, **kw)
