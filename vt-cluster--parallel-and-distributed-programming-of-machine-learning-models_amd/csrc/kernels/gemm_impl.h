@@ -2575,10 +2575,12 @@ std::vector<at::Tensor> lmhead_fwd_impl(const at::Tensor& a, const at::Tensor& w
     // tile raster of the head: the 32 blocks an XCD runs at once cover g row panels x 32/g vocab tiles,
     // so each W tile is fetched from the Infinity Cache once per g row panels (row-panel order, g = 1,
     // fetched 2.5 GB per distilgpt2 forward: FETCH_SIZE, profiles/r5/pmc_roofline_distilgpt2_step.txt);
-    // persistent kernel measured g = 4 best at K = 768 (648 vs 714 us), g = 8 at K = 2560 (1381 vs 1491)
-    // (profiles/r5/bench_lm_persist.jsonl).  MIFT_LM_GROUP (per call) overrides.
+    // persistent kernel measured g = 4 best at K = 768 in isolation (648 vs 714 us), g = 8 at K = 2560
+    // (1381 vs 1491) (profiles/r5/bench_lm_persist.jsonl); inside the distilgpt2 step g = 3 is best
+    // (4.630 vs 4.649 / 4.660 / 4.731 ms for g = 2 / 4 / 1, profiles/r6/step_ab_dgpt_lm_group*.json).
+    // MIFT_LM_GROUP (per call) overrides.
     const char* g = getenv("MIFT_LM_GROUP");
-    ep.group_m = g ? atoi(g) : (K <= 1024 ? 4 : 8);
+    ep.group_m = g ? atoi(g) : (K <= 1024 ? 3 : 8);
   }
   SkArgs sk{};
   // staging ring (128 KiB) reused for the E tile + the two row-partial arrays
