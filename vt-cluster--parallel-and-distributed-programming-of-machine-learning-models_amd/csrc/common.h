@@ -165,6 +165,36 @@ MIFT_HD float gelu_erf_grad(float x) {
   return cdf + x * pdf;
 }
 
+// Lanes l and l ^ 16 (l ^ 32) combined through gfx950's v_permlane16_swap (v_permlane32_swap): a VALU
+// exchange, where __shfl_xor at these distances is a ds_bpermute_b32 LDS round trip plus its lgkmcnt
+// wait.  The swap of a register with itself leaves {own, partner} in the two results (in a
+// lane-dependent order); max / + / | are commutative, so the results equal the __shfl_xor forms bit
+// for bit.
+MIFT_HD float xor16_max(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+MIFT_HD float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+MIFT_HD float xor16_add(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+MIFT_HD float xor32_add(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+MIFT_HD uint32_t xor16_or(uint32_t x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return (uint32_t)r[0] | (uint32_t)r[1];
+}
+MIFT_HD uint32_t xor32_or(uint32_t x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (uint32_t)r[0] | (uint32_t)r[1];
+}
+
 // wave64 reductions (DPP/shuffle handled by the compiler for __shfl_xor).
 MIFT_HD float wave_sum(float v) {
 #pragma unroll

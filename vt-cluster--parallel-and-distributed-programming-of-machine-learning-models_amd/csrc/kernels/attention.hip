@@ -316,8 +316,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
           st[j][t][r] = v;
           tmax = fmaxf(tmax, v);
         }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = xor16_max(tmax);
+      tmax = xor32_max(tmax);
       // lazy rescale: the running max only moves when some row's tile max exceeds it by
       // > 2^8 (p <= 256 stays exact in fp32 and representable in bf16/fp16), so most tiles
       // skip the O rescale and its accumulator round trips (wave-uniform branch)
@@ -374,8 +374,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const T* __restrict__ qkv
 #pragma unroll
   for (int j = 0; j < QG; ++j) {
     float lj = l[j];
-    lj += __shfl_xor(lj, 16, 64);
-    lj += __shfl_xor(lj, 32, 64);
+    lj = xor16_add(lj);
+    lj = xor32_add(lj);
     const float inv_l = lj > 0.f ? 1.f / lj : 0.f;
     const int q0j = q0 + 16 * j, myq = q0j + qc;
     if (g == 0 && myq < S) lse[(int64_t)bh * S + myq] = (lj > 0.f) ? (m[j] + log2f(lj)) * LN2 : -INFINITY;
@@ -615,8 +615,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
           st[t][r] = v;
           tmax = fmaxf(tmax, v);
         }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = xor16_max(tmax);
+      tmax = xor32_max(tmax);
       const bool resc = __any(tmax > m + 8.f);
       float alpha = 1.f;
       if (resc) {
@@ -650,8 +650,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
         // k0 + 16t + j); the four g-lanes of a query each own one nibble of every element
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
-          kbits[h2] |= __shfl_xor(kbits[h2], 16, 64);
-          kbits[h2] |= __shfl_xor(kbits[h2], 32, 64);
+          kbits[h2] = xor16_or(kbits[h2]);
+          kbits[h2] = xor32_or(kbits[h2]);
         }
         if (g == 0 && myq < S)
           *reinterpret_cast<uint2*>(dmask + ((int64_t)bh * S + myq) * NR + kt * 4) = make_uint2(kbits[0], kbits[1]);
@@ -680,8 +680,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_fwd_seq_kernel
     };
     for (int kt = 0; kt + 1 < nkt; ++kt) ktile(kt, std::false_type{});
     if (nkt > 0) ktile(nkt - 1, std::true_type{});
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    l = xor16_add(l);
+    l = xor32_add(l);
     const float inv_l = l > 0.f ? 1.f / l : 0.f;
     if (g == 0 && myq < S) lse[(int64_t)bh * S + myq] = (l > 0.f) ? (m + log2f(l)) * LN2 : -INFINITY;
     if constexpr (OT) {
@@ -755,8 +755,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const T* __restrict__ 
     for (int s = 0; s < G::NKS; ++s)
 #pragma unroll
       for (int e = 0; e < 8; ++e) Dq += (float)of[s][e] * (float)df[s][e];
-    Dq += __shfl_xor(Dq, 16, 64);
-    Dq += __shfl_xor(Dq, 32, 64);
+    Dq = xor16_add(Dq);
+    Dq = xor32_add(Dq);
     if (g == 0 && myq < S) Dv[(int64_t)bh * S + myq] = Dq;
   }
   const float lse2 = myq < S ? lse[(int64_t)bh * S + myq] * LOG2E : 0.f;
@@ -1087,8 +1087,8 @@ __global__ __launch_bounds__(NW * 64, HD <= 80 ? 4 : 2) void attn_bwd_dq_seq_ker
       for (int s = 0; s < G::NKS; ++s)
 #pragma unroll
         for (int e = 0; e < 8; ++e) Dq += (float)of[s][e] * (float)df[s][e];
-      Dq += __shfl_xor(Dq, 16, 64);
-      Dq += __shfl_xor(Dq, 32, 64);
+      Dq = xor16_add(Dq);
+      Dq = xor32_add(Dq);
       if (g == 0 && myq < S) Dv[(int64_t)bh * S + myq] = Dq;
     }
     const float lse2 = myq < S ? lse[(int64_t)bh * S + myq] * LOG2E : 0.f;

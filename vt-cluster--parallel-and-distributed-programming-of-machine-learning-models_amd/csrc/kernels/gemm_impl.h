@@ -1248,8 +1248,8 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
 #pragma unroll
           for (int e = 0; e < 4; ++e) m = (FULL || col + e < V) ? fmaxf(m, acc[i][j][e]) : m;
         }
-        m = fmaxf(m, __shfl_xor(m, 16, 64));
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        m = xor16_max(m);
+        m = xor32_max(m);
         if (fq == 0) redm[wave * WM + i * 16 + fr] = m;
       }
       __syncthreads();
@@ -1285,8 +1285,8 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
           store4<T>(Cs + CT::off4(lrow, lcol), ev);
         }
         if (hit) lm.zlab[row] = zl;
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
+        s = xor16_add(s);
+        s = xor32_add(s);
         if (fq == 0) reds[wave * WM + i * 16 + fr] = s;
       }
     };
@@ -1623,8 +1623,8 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
 #pragma unroll
         for (int e = 0; e < 4; ++e) m = (FULL || col + e < V) ? fmaxf(m, acc[i][j][e]) : m;
       }
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      m = xor16_max(m);
+      m = xor32_max(m);
       if (fq == 0) redm[wave * WM + i * 16 + fr] = m;
     }
     raw_barrier();
@@ -1660,8 +1660,8 @@ __global__ __launch_bounds__(512) void lmhead_fwd_persist_kernel(const T* __rest
         pk[j][1] = pack2(ev[2], ev[3]);
       }
       if (hit && row < M) lm.zlab[row] = zl;
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      s = xor16_add(s);
+      s = xor32_add(s);
       if (fq == 0) reds[wave * WM + i * 16 + fr] = s;
       // lanes l (row quarter fq even) and l ^ 16 trade fragments: fq even ends with columns
       // 32p + 8(fq>>1) .. +7, fq odd with 32p + 16 + 8(fq>>1) .. +7 of the wave's 64
@@ -2069,8 +2069,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const T* __restric
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        ps[i] += __shfl_xor(ps[i], 16, 64);
-        ps[i] += __shfl_xor(ps[i], 32, 64);
+        ps[i] = xor16_add(ps[i]);
+        ps[i] = xor32_add(ps[i]);
       }
       if (fq == 0) {
 #pragma unroll

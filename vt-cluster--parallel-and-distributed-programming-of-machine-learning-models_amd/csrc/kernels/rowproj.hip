@@ -272,8 +272,8 @@ __global__ __launch_bounds__(NW * 64) void rowproj_mfma_kernel(const T* __restri
   T* yr = y + (size_t)row * D + c00;
   // sum over the block's NW waves (in wave order) of a per-row value held by lanes g = 0..3 of every wave
   auto row_sum = [&](float v) {
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
+    v = xor16_add(v);
+    v = xor32_add(v);
     if (g == 0) red[wave][fr] = v;
     __syncthreads();
     float r = 0.f;
@@ -365,10 +365,10 @@ __global__ __launch_bounds__(NW * 64) void rowproj_mfma_kernel(const T* __restri
     }
     {  // both row sums in one LDS exchange (one barrier pair instead of two)
       __shared__ float red2[NW][16][2];
-      sg += __shfl_xor(sg, 16, 64);
-      sg += __shfl_xor(sg, 32, 64);
-      sgx += __shfl_xor(sgx, 16, 64);
-      sgx += __shfl_xor(sgx, 32, 64);
+      sg = xor16_add(sg);
+      sg = xor32_add(sg);
+      sgx = xor16_add(sgx);
+      sgx = xor32_add(sgx);
       if (g == 0) {
         red2[wave][fr][0] = sg;
         red2[wave][fr][1] = sgx;
