@@ -195,7 +195,7 @@ def _partition_halves(n_layers, n_stages, head, embed, ranks, attn_frac):
         b.append(j)
     b.append(nu)
     best = score(b)
-    for _ in range(4 * nu):  # moves: shift any run of consecutive boundaries by one unit
+    for _ in range(64):  # moves: shift any run of consecutive boundaries by one unit (converges in a few)
         improved = False
         for k1 in range(1, n_stages):
             for k2 in range(k1, n_stages):
