@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="8,10")
     ap.add_argument("--shapes", default="opt", help="opt | dgpt (the K = 768 distilgpt2 block GEMMs, bf16)")
+    ap.add_argument("--ext", action="store_true", help="also time each shape with a LoRA K-extension (a2/b2)")
     a = ap.parse_args()
     import mift._C as C
     if a.shapes == "dgpt":
@@ -32,18 +33,21 @@ def main():
         x = torch.randn(M, K, device="cuda", dtype=dt)
         w = torch.randn(N, K, device="cuda", dtype=dt)
         nblk = ((M + 63) // 64) * ((N + 63) // 64)  # >= the block count of any tile
-        for tile in [int(t) for t in a.tiles.split(",")]:
-            for store in (1, 0):
+        a2 = torch.randn(M, 32, device="cuda", dtype=dt)
+        b2 = torch.randn(N, 32, device="cuda", dtype=dt)
+        for tile, ext in [(int(t), e) for t in a.tiles.split(",") for e in ((0, 1) if a.ext else (0,))]:
+            for store in ((1,) if a.ext else (1, 0)):
                 os.environ["MIFT_LM_DBG"] = "0" if store else "1"
                 buf = torch.zeros(nblk * 8, dtype=torch.int64, device="cuda")
                 C.gemm_set_stamps(buf)
                 for _ in range(3):
-                    C.gemm_nt(x, w, None, None, None, 0, None, None, 0.0, 0, False, 1.0, None, tile, None, None, 0.0, 0)
+                    C.gemm_nt(x, w, None, a2 if ext else None, b2 if ext else None, 0, None, None, 0.0, 0, False, 1.0,
+                              None, tile, None, None, 0.0, 0)
                 torch.cuda.synchronize()
                 C.gemm_set_stamps(None)
                 s = [b for b in buf.view(nblk, 8).cpu().tolist() if b[0] != 0]  # launched blocks only
                 med = lambda v: statistics.median(v)  # noqa: E731
-                row = {"shape": f"{M}x{N}x{K}", "tile": tile, "c_store": bool(store), "blocks": len(s)}
+                row = {"shape": f"{M}x{N}x{K}", "tile": tile, "ext": bool(ext), "c_store": bool(store), "blocks": len(s)}
                 if tile == 10:
                     row["prologue_cyc"] = med([b[1] - b[0] for b in s])
                     row["loop_cyc"] = med([b[2] - b[1] for b in s])

@@ -144,6 +144,7 @@ struct EpiArgs {
   long long* stamps;
   int staged;     // interior tiles: feature-staged epilogue phase 2 (MIFT_EPI_STAGED, default 1)
   int hoist;      // dropout-mask hashes with the hoisted high-word mix (output < 2^33 elements; MIFT_EPI_HOIST)
+  int ext_lds;    // NSTAGE >= 2 tiles: K-extension operands staged into LDS during the last k-tile (MIFT_EXT_LDS)
 };
 
 // Tile t (after the XCD remap, consecutive t share an XCD) -> (row tile, column tile).  With g > 0
@@ -448,8 +449,31 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
   const int fr = lane & 15;  // fragment row
   const int fq = lane >> 4;  // k sub-chunk (0..3)
 
-  // acc = sum over k-tiles [kb, ke) of the (m0, n0) tile
-  auto mainloop = [&](int kb, int ke) {
+  // LoRA K-extension operands (A2 [M, 32], B2 [N, 32]: 64-B rows) of this tile staged into a free ring
+  // buffer by LDS-DMA during the last k-tile, so the epilogue reads them from LDS instead of waiting a
+  // global round trip after the main loop (epilogue phase 1 with the extension +1.2k-2.0k -> +0.5k-0.8k
+  // cycles per block, profiles/r6/gemm_stamps_dgpt_ext_{global,lds}.txt; distilgpt2 step 4.680 -> 4.666 ms
+  // same-process, step_ab_dgpt_ext_lds.json).  1-KiB pieces of 16 rows; lane -> (row 16p + lane/4, physical 16-B chunk lane%4) holding
+  // logical chunk phys ^ ((row >> 2) & 3), so a fragment read (16 rows, one logical chunk) spreads
+  // over all 64 banks.
+  constexpr int EXT_PA = BM / 16, EXT_PB = BN / 16;
+  int ext_buf = -1;  // ring buffer holding the staged K-extension operands (-1: not staged)
+  auto stage_ext = [&](int buf) {
+    char* base = smem + buf * STAGE_BYTES;
+    const int row = lane >> 2, phys = lane & 3;
+    for (int p = wave; p < EXT_PA + EXT_PB; p += NW) {  // wave-uniform
+      const bool isa = p < EXT_PA;
+      const int r = (isa ? p : p - EXT_PA) * 16 + row;
+      const int lc = phys ^ ((r >> 2) & 3);
+      const T* src = isa ? A2 + (size_t)min(m0 + r, M - 1) * 32 : B2 + (size_t)min(n0 + r, N - 1) * 32;
+      __builtin_amdgcn_global_load_lds((const void*)(src + lc * 8), (void*)(base + p * 1024), 16, 0, 0);
+    }
+  };
+  static_assert(NSTAGE < 2 || (BM % 16 == 0 && BN % 16 == 0 && (BM + BN) * 64 <= STAGE_BYTES),
+                "K-extension staging: 16-row pieces fit one ring buffer");
+
+  // acc = sum over k-tiles [kb, ke) of the (m0, n0) tile; extl: stage the K-extension operands too
+  auto mainloop = [&](int kb, int ke, bool extl = false) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -478,6 +502,10 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
       __builtin_amdgcn_s_barrier();  // everyone's pieces of kt landed; everyone done reading kt-1
       asm volatile("" ::: "memory");  // no LDS access may move above the barrier
       if (kt + NBUF - 1 < nk) stage((kt + NBUF - 1) % NBUF, (kb + kt + NBUF - 1) * KB);
+      else if (extl && kt == nk - 1) {  // that buffer held tile kt-1, read by everyone before the barrier
+        ext_buf = (kt + NBUF - 1) % NBUF;
+        stage_ext(ext_buf);
+      }
       const char* As = smem + (kt % NBUF) * STAGE_BYTES;
       const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -773,7 +801,23 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
     // ---- LoRA K-extension: one extra K=32 step from global (A2[M,32], B2[N,32]) ----
     frag_t<T> af2[TM], bf2[TN];
     const bool ext = A2 != nullptr;
-    if (ext) {
+    if (ext && ext_buf >= 0) {  // staged by the main loop's last k-tile (NSTAGE >= 2 data-parallel tiles)
+      wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's pieces landed
+      asm volatile("" ::: "memory");
+      const char* eb = smem + ext_buf * STAGE_BYTES;
+  #pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WM + i * 16 + fr;
+        af2[i] = *reinterpret_cast<const frag_t<T>*>(eb + r * 64 + ((fq ^ ((r >> 2) & 3)) << 4));
+      }
+  #pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WN + j * 16 + fr;
+        bf2[j] = *reinterpret_cast<const frag_t<T>*>(eb + BM * 64 + r * 64 + ((fq ^ ((r >> 2) & 3)) << 4));
+      }
+    } else if (ext) {
   #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = min(m0 + wm * WM + i * 16 + fr, M - 1);
@@ -784,6 +828,8 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
         const int r = min(n0 + wn * WN + j * 16 + fr, N - 1);
         bf2[j] = *reinterpret_cast<const frag_t<T>*>(B2 + (size_t)r * 32 + fq * 8);
       }
+    }
+    if (ext) {
       if (ep.ext_thr == 0) {
   #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -1451,7 +1497,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
     } else if constexpr (NSTAGE == 1) {
       mainloop4(0, nk_all);
     } else {
-      mainloop(0, nk_all);
+      mainloop(0, nk_all, A2 != nullptr && ep.ext_lds);
     }
     stamp(2);
     epilogue();
@@ -2877,6 +2923,8 @@ std::vector<at::Tensor> mift_gemm_nt(const at::Tensor& a, const at::Tensor& b, c
     ep.staged = e ? atoi(e) : 1;
     const char* h = getenv("MIFT_EPI_HOIST");   // read per call (A/B); needs M·N < 2^33
     ep.hoist = (h ? atoi(h) : 1) && (uint64_t)M * N < (1ull << 33);
+    const char* x = getenv("MIFT_EXT_LDS");     // read per call (A/B)
+    ep.ext_lds = x ? atoi(x) : 1;
   }
   ep.sbits = nullptr;
   if (sbits) {  // ReLU sign bits: written (act = relu) or read in place of aux (act = relu backward)
