@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--tiles", default="8,10")
     ap.add_argument("--shapes", default="opt", help="opt | dgpt (the K = 768 distilgpt2 block GEMMs, bf16)")
     ap.add_argument("--ext", action="store_true", help="also time each shape with a LoRA K-extension (a2/b2)")
+    ap.add_argument("--bias", action="store_true", help="with --ext: the variants add a bias instead")
     a = ap.parse_args()
     import mift._C as C
     if a.shapes == "dgpt":
@@ -33,6 +34,7 @@ def main():
         x = torch.randn(M, K, device="cuda", dtype=dt)
         w = torch.randn(N, K, device="cuda", dtype=dt)
         nblk = ((M + 63) // 64) * ((N + 63) // 64)  # >= the block count of any tile
+        bias = torch.randn(N, device="cuda", dtype=dt)
         a2 = torch.randn(M, 32, device="cuda", dtype=dt)
         b2 = torch.randn(N, 32, device="cuda", dtype=dt)
         for tile, ext in [(int(t), e) for t in a.tiles.split(",") for e in ((0, 1) if a.ext else (0,))]:
@@ -41,8 +43,12 @@ def main():
                 buf = torch.zeros(nblk * 8, dtype=torch.int64, device="cuda")
                 C.gemm_set_stamps(buf)
                 for _ in range(3):
-                    C.gemm_nt(x, w, None, a2 if ext else None, b2 if ext else None, 0, None, None, 0.0, 0, False, 1.0,
-                              None, tile, None, None, 0.0, 0)
+                    if a.bias:
+                        C.gemm_nt(x, w, bias if ext else None, None, None, 0, None, None, 0.0, 0, False, 1.0,
+                                  None, tile, None, None, 0.0, 0)
+                    else:
+                        C.gemm_nt(x, w, None, a2 if ext else None, b2 if ext else None, 0, None, None, 0.0, 0, False,
+                                  1.0, None, tile, None, None, 0.0, 0)
                 torch.cuda.synchronize()
                 C.gemm_set_stamps(None)
                 s = [b for b in buf.view(nblk, 8).cpu().tolist() if b[0] != 0]  # launched blocks only
