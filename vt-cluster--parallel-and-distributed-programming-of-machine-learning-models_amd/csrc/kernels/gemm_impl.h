@@ -458,19 +458,32 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
   // over all 64 banks.
   constexpr int EXT_PA = BM / 16, EXT_PB = BN / 16;
   int ext_buf = -1;  // ring buffer holding the staged K-extension operands (-1: not staged)
+  // The bias row of the tile rides along (one 1-KiB piece after the extension rows, bytes
+  // [n0·esz, n0·esz + 1024) of the bias; lanes past the end re-read its last 16 B, which only feed
+  // columns >= N): phase 1 read it from global after the main loop, +0.8k-1.5k cycles per block.
+  constexpr int EXT_BIAS_OFF = (BM + BN) * 64;
+  const int besz = ep.bias_f32 ? 4 : 2;
+  const bool bias_lds = ep.bias != nullptr && ((size_t)N * besz) % 16 == 0 && BN * 4 <= 1024;
   auto stage_ext = [&](int buf) {
     char* base = smem + buf * STAGE_BYTES;
     const int row = lane >> 2, phys = lane & 3;
-    for (int p = wave; p < EXT_PA + EXT_PB; p += NW) {  // wave-uniform
-      const bool isa = p < EXT_PA;
-      const int r = (isa ? p : p - EXT_PA) * 16 + row;
-      const int lc = phys ^ ((r >> 2) & 3);
-      const T* src = isa ? A2 + (size_t)min(m0 + r, M - 1) * 32 : B2 + (size_t)min(n0 + r, N - 1) * 32;
-      __builtin_amdgcn_global_load_lds((const void*)(src + lc * 8), (void*)(base + p * 1024), 16, 0, 0);
+    if (A2 != nullptr) {
+      for (int p = wave; p < EXT_PA + EXT_PB; p += NW) {  // wave-uniform
+        const bool isa = p < EXT_PA;
+        const int r = (isa ? p : p - EXT_PA) * 16 + row;
+        const int lc = phys ^ ((r >> 2) & 3);
+        const T* src = isa ? A2 + (size_t)min(m0 + r, M - 1) * 32 : B2 + (size_t)min(n0 + r, N - 1) * 32;
+        __builtin_amdgcn_global_load_lds((const void*)(src + lc * 8), (void*)(base + p * 1024), 16, 0, 0);
+      }
+    }
+    if (bias_lds && wave == NW - 1) {
+      const size_t off = min((size_t)n0 * besz + (size_t)lane * 16, (size_t)N * besz - 16);
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(ep.bias) + off),
+                                       (void*)(base + EXT_BIAS_OFF), 16, 0, 0);
     }
   };
-  static_assert(NSTAGE < 2 || (BM % 16 == 0 && BN % 16 == 0 && (BM + BN) * 64 <= STAGE_BYTES),
-                "K-extension staging: 16-row pieces fit one ring buffer");
+  static_assert(NSTAGE < 2 || (BM % 16 == 0 && BN % 16 == 0 && (BM + BN) * 64 + 1024 <= STAGE_BYTES),
+                "K-extension / bias staging: 16-row pieces and the bias piece fit one ring buffer");
 
   // acc = sum over k-tiles [kb, ke) of the (m0, n0) tile; extl: stage the K-extension operands too
   auto mainloop = [&](int kb, int ke, bool extl = false) {
@@ -801,11 +814,28 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
     // ---- LoRA K-extension: one extra K=32 step from global (A2[M,32], B2[N,32]) ----
     frag_t<T> af2[TM], bf2[TN];
     const bool ext = A2 != nullptr;
-    if (ext && ext_buf >= 0) {  // staged by the main loop's last k-tile (NSTAGE >= 2 data-parallel tiles)
+    float bpre[TN][4];  // the tile's bias columns, read from the staged piece before the ring is reused
+    const bool bias_pre = bias_lds && ext_buf >= 0;
+    if (ext_buf >= 0) {  // staged by the main loop's last k-tile (NSTAGE >= 2 data-parallel tiles)
       wait_vmcnt<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's pieces landed
       asm volatile("" ::: "memory");
+    }
+    if (bias_pre) {
+      const char* bb = smem + ext_buf * STAGE_BYTES + EXT_BIAS_OFF;
+  #pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + fq * 4;
+        if (ep.bias_f32) {
+          const float4 t4 = *reinterpret_cast<const float4*>(bb + col * 4);
+          bpre[j][0] = t4.x; bpre[j][1] = t4.y; bpre[j][2] = t4.z; bpre[j][3] = t4.w;
+        } else {
+          load4<T>(reinterpret_cast<const T*>(bb) + col, bpre[j]);
+        }
+      }
+    }
+    if (ext && ext_buf >= 0) {
       const char* eb = smem + ext_buf * STAGE_BYTES;
   #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -855,7 +885,12 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
       for (int j = 0; j < TN; ++j) {
         const int col = wn * WN + j * 16 + fq * 4;
         float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (ep.bias != nullptr && n0 + col < N) {
+        if (bias_pre) {
+          if (n0 + col < N) {
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) bv[e] = bpre[j][e];
+          }
+        } else if (ep.bias != nullptr && n0 + col < N) {
           if (ep.bias_f32) {
             float4 t4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ep.bias) + n0 + col);
             bv[0] = t4.x; bv[1] = t4.y; bv[2] = t4.z; bv[3] = t4.w;
@@ -1497,7 +1532,7 @@ __global__ __launch_bounds__(NWM* NWN * 64, (gemm_waves_per_eu<BM, BN, NWM, NWN,
     } else if constexpr (NSTAGE == 1) {
       mainloop4(0, nk_all);
     } else {
-      mainloop(0, nk_all, A2 != nullptr && ep.ext_lds);
+      mainloop(0, nk_all, (A2 != nullptr || bias_lds) && ep.ext_lds);
     }
     stamp(2);
     epilogue();
